@@ -1,0 +1,267 @@
+"""fp64 CPU restatement of the pycwt 0.4.0b0 numerics the reference calls.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product path (``wavelet-transformer_amd/``)
+imports this module; only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may use it, and only as the checker / the
+timed CPU baseline.
+
+Provenance and pinning
+----------------------
+pycwt==0.4.0b0 (pinned at reference ``requirements.txt:33``, ``uv.lock:874-886``) is
+NOT present in this container and cannot be fetched (no network).  This file
+restates its published algorithm (Torrence & Compo 1998; Grinsted et al. 2004;
+pycwt ``wavelet.py`` / ``mothers.py`` / ``helpers.py``) as summarised in
+SURVEY.md Appendix A, using the same scipy primitives pycwt uses when pyfftw is
+absent (``scipy.fftpack.fft/ifft/fftfreq``, ``scipy.signal.convolve2d``,
+``scipy.stats.chi2``).
+
+**Parity for CWT / XWT / WCT / AR(1) / significance is UNPINNED**: the reference's
+own tests assert lengths only (``tests/test_cwt.py:30,34``, ``tests/test_xwt.py:48,53``).
+The restatement is pinned by the analytic known-answer tests of SURVEY.md A.6
+(``tests/test_oracle_cwt.py``).
+
+Reference call sites (what these functions stand in for):
+  * ``cwt``          <- ``src/cwt.py:110``, inside ``xwt``/``wct``
+  * ``ar1``          <- ``src/cwt.py:106``
+  * ``significance`` <- ``src/cwt.py:123-131``
+  * ``xwt``          <- ``src/xwt.py:93-101``
+  * ``wct``          <- ``src/wct.py:106-118``, ``src/xwt.py:122-134``
+"""
+
+from __future__ import annotations
+
+import numpy as np
+from scipy import fftpack
+from scipy.signal import convolve2d
+from scipy.stats import chi2
+
+
+class Morlet:
+    """Morlet mother wavelet, pycwt ``mothers.Morlet``.
+
+    Used by the reference as ``pycwt.Morlet(f0=6)`` (``src/cwt.py:44``,
+    ``constants/results_configs.py:31,54``).
+    """
+
+    name = "Morlet"
+
+    def __init__(self, f0: float = 6.0):
+        self.f0 = float(f0)
+        self.dofmin = 2
+        if self.f0 == 6:
+            self.cdelta = 0.776
+            self.gamma = 2.32
+            self.deltaj0 = 0.60
+        else:
+            self.cdelta = -1
+            self.gamma = -1
+            self.deltaj0 = -1
+
+    def psi_ft(self, f):
+        # No Heaviside step: negative frequencies contribute (A.1).
+        return (np.pi ** -0.25) * np.exp(-0.5 * (f - self.f0) ** 2)
+
+    def flambda(self):
+        return (4 * np.pi) / (self.f0 + np.sqrt(2 + self.f0 ** 2))
+
+    def coi(self):
+        return 1.0 / np.sqrt(2)
+
+    def smooth(self, W, dt, dj, scales):
+        """Time Gaussian (via FFT) then scale boxcar, SURVEY A.4 ``Morlet.smooth``."""
+        m, n = W.shape
+        npad = next_pow2(n)
+        k = 2 * np.pi * fftpack.fftfreq(npad)
+        k2 = k ** 2
+        snorm = scales / dt
+        F = np.exp(-0.5 * (snorm[:, np.newaxis] ** 2) * k2)
+        smooth = fftpack.ifft(F * fftpack.fft(W, axis=1, n=npad), axis=1, n=npad)
+        T = smooth[:, :n]
+        if np.isreal(W).all():
+            T = T.real
+        wsize = self.deltaj0 / dj * 2
+        win = rect(int(np.round(wsize)), normalize=True)
+        return convolve2d(T, win[:, np.newaxis], "same")
+
+
+def rect(x: int, normalize: bool = False) -> np.ndarray:
+    """Boxcar with half-weight end points (pycwt ``helpers.rect``)."""
+    X = np.zeros(x)
+    X[0] = X[-1] = 0.5
+    X[1:-1] = 1
+    if normalize:
+        X /= X.sum()
+    return X
+
+
+def next_pow2(n: int) -> int:
+    """pycwt ``helpers.fft_kwargs``: FFT length = 2**ceil(log2(n))."""
+    return int(2 ** np.ceil(np.log2(n)))
+
+
+def scales_for(n0: int, dt: float, dj: float, s0: float, J: float, wavelet: Morlet):
+    """Default-parameter resolution of pycwt ``cwt``."""
+    if s0 == -1:
+        s0 = 2 * dt / wavelet.flambda()
+    if J == -1:
+        J = int(np.round(np.log2(n0 * dt / s0) / dj))
+    sj = s0 * 2 ** (np.arange(0, J + 1) * dj)
+    freqs = 1 / (wavelet.flambda() * sj)
+    return sj, freqs
+
+
+def cwt(signal, dt, dj=1 / 12, s0=-1, J=-1, wavelet=None):
+    """pycwt ``cwt``: FFT convolution with the analytic Morlet.
+
+    Returns ``(W[:, :n0], sj, freqs, coi, signal_ft[1:N//2]/sqrt(N), ftfreqs[1:N//2]/2pi)``.
+    """
+    wavelet = wavelet or Morlet(6)
+    signal = np.asarray(signal)
+    n0 = len(signal)
+    sj, freqs = scales_for(n0, dt, dj, s0, J, wavelet)
+    N = next_pow2(n0)
+    signal_ft = fftpack.fft(signal, n=N)
+    ftfreqs = 2 * np.pi * fftpack.fftfreq(N, dt)
+    sj_col = sj[:, np.newaxis]
+    psi_ft_bar = (sj_col * ftfreqs[1] * N) ** 0.5 * np.conjugate(
+        wavelet.psi_ft(sj_col * ftfreqs)
+    )
+    W = fftpack.ifft(signal_ft * psi_ft_bar, axis=1, n=N)
+    sel = np.invert(np.isnan(W).all(axis=1))
+    if np.any(sel):
+        sj = sj[sel]
+        freqs = freqs[sel]
+        W = W[sel, :]
+    coi = n0 / 2 - np.abs(np.arange(0, n0) - (n0 - 1) / 2)
+    coi = wavelet.flambda() * wavelet.coi() * dt * coi
+    return (
+        W[:, :n0],
+        sj,
+        freqs,
+        coi,
+        signal_ft[1 : N // 2] / N ** 0.5,
+        ftfreqs[1 : N // 2] / (2 * np.pi),
+    )
+
+
+def ar1(x):
+    """Unbiased AR(1) estimate after Grinsted.
+
+    Raises the built-in ``Warning`` when no upper bound exists; the reference
+    app relies on catching it (``src/wavelet_plots.py:684``).
+    """
+    x = np.asarray(x)
+    N = x.size
+    xm = x.mean()
+    x = x - xm
+    c0 = x.transpose().dot(x) / len(x)
+    c1 = x[0 : N - 1].transpose().dot(x[1:N]) / (N - 1)
+    B = -c1 * N - c0 * N ** 2 - 2 * c0 + 2 * c1 - c1 * N ** 2 + c0 * N
+    A = c0 * N ** 2
+    C = N * (c0 + c1 * N - c1)
+    D = B ** 2 - 4 * A * C
+    if D > 0:
+        g = (-B - D ** 0.5) / (2 * A)
+    else:
+        raise Warning(
+            "Cannot place an upperbound on the unbiased AR(1). "
+            "Series is too short or trend is to large."
+        )
+    mu2 = -1 / N + (2 / N ** 2) * (
+        (N - g ** N) / (1 - g) - g * (1 - g ** (N - 1)) / (1 - g) ** 2
+    )
+    c0t_pos = c0 / (1 - mu2)
+    a = ((1 - g ** 2) * c0t_pos) ** 0.5
+    return g, a, mu2
+
+
+def ar1_spectrum(freqs, ar1=0.0):
+    freqs = np.asarray(freqs)
+    return (1 - ar1 ** 2) / np.abs(1 - ar1 * np.exp(-2 * np.pi * 1j * freqs)) ** 2
+
+
+def significance(signal, dt, scales, sigma_test=0, alpha=None,
+                 significance_level=0.95, dof=-1, wavelet=None):
+    """pycwt ``significance`` for ``sigma_test == 0`` (the only form the reference uses,
+    ``src/cwt.py:123-131``)."""
+    wavelet = wavelet or Morlet(6)
+    try:
+        n0 = len(signal)
+    except TypeError:
+        n0 = 1
+    if n0 == 1:
+        variance = signal
+    else:
+        variance = np.asarray(signal).std() ** 2
+    if alpha is None:
+        alpha, _, _ = ar1(signal)
+    period = scales * wavelet.flambda()
+    freq = dt / period
+    dofmin = wavelet.dofmin
+    fft_theor = (1 - alpha ** 2) / (1 + alpha ** 2 - 2 * alpha * np.cos(2 * np.pi * freq))
+    fft_theor = variance * fft_theor
+    if sigma_test != 0:
+        raise NotImplementedError("only sigma_test=0 is used by the reference")
+    dof = dofmin
+    chisquare = chi2.ppf(significance_level, dof) / dof
+    signif = fft_theor * chisquare
+    return signif, fft_theor
+
+
+def _normalized(y1, y2, normalize):
+    y1 = np.asarray(y1)
+    y2 = np.asarray(y2)
+    std1 = y1.std()
+    std2 = y2.std()
+    if normalize:
+        return y1, y2, (y1 - y1.mean()) / std1, (y2 - y2.mean()) / std2, std1, std2
+    return y1, y2, y1, y2, std1, std2
+
+
+def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95,
+        wavelet=None, normalize=True):
+    """pycwt ``xwt``. Returns ``(W12, coi, freq, signif)``."""
+    wavelet = wavelet or Morlet(6)
+    y1, y2, y1n, y2n, std1, std2 = _normalized(y1, y2, normalize)
+    kw = dict(dj=dj, s0=s0, J=J, wavelet=wavelet)
+    W1, sj, freq, coi, _, _ = cwt(y1n, dt, **kw)
+    W2, sj, freq, coi, _, _ = cwt(y2n, dt, **kw)
+    W12 = W1 * W2.conj()
+    if normalize:
+        std1 = std2 = 1.0
+    a1, _, _ = ar1(y1)
+    a2, _, _ = ar1(y2)
+    Pk1 = ar1_spectrum(freq * dt, a1)
+    Pk2 = ar1_spectrum(freq * dt, a2)
+    dof = wavelet.dofmin
+    PPF = chi2.ppf(significance_level, dof)
+    signif = std1 * std2 * (Pk1 * Pk2) ** 0.5 * PPF / dof
+    return W12, coi, freq, signif
+
+
+def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
+        wavelet=None, normalize=True, **kwargs):
+    """pycwt ``wct`` with ``sig=False``.
+
+    ``**kwargs`` swallows ``cache=`` and ``delta_j=`` exactly as pycwt does
+    (reference quirk B.5: ``src/xwt.py:126`` passes ``delta_j=`` and so runs at
+    the default dj=1/12).  The Monte-Carlo ``wct_significance`` (sig=True) is
+    SURVEY §8(f) row 1 and not restated here.
+    """
+    wavelet = wavelet or Morlet(6)
+    if np.asarray(y1).size != np.asarray(y2).size:
+        raise AssertionError("Input signals must have the same size")
+    y1, y2, y1n, y2n, _, _ = _normalized(y1, y2, normalize)
+    kw = dict(dj=dj, s0=s0, J=J, wavelet=wavelet)
+    W1, sj, freq, coi, _, _ = cwt(y1n, dt, **kw)
+    W2, sj, freq, coi, _, _ = cwt(y2n, dt, **kw)
+    scales = np.ones([1, y1.size]) * sj[:, None]
+    S1 = wavelet.smooth(np.abs(W1) ** 2 / scales, dt, dj, sj)
+    S2 = wavelet.smooth(np.abs(W2) ** 2 / scales, dt, dj, sj)
+    W12 = W1 * W2.conj()
+    S12 = wavelet.smooth(W12 / scales, dt, dj, sj)
+    WCT = np.abs(S12) ** 2 / (S1 * S2)
+    aWCT = np.angle(W12)
+    if sig:
+        raise NotImplementedError("wct_significance (Monte Carlo) is SURVEY 8(f) row 1")
+    return WCT, aWCT, coi, freq, np.asarray([0])
