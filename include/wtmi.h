@@ -1,0 +1,109 @@
+/*
+ * wtmi.h -- C ABI of the MI355X wavelet-transform engine (libwtmi.so).
+ *
+ * Drop-in boundary for the numerics behind the reference's src.cwt / src.xwt /
+ * src.wct / src.dwt / src.modwt modules.  The reference is pure Python; each entry
+ * point below replaces a third-party call made from those modules (file:line into
+ * the reference tree).  The Python host layer binds these with ctypes
+ * (wavelet-transformer_amd/wtmi/_lib.py).
+ *
+ * Conventions (all entry points):
+ *   - every array pointer is a DEVICE pointer (hipMalloc / torch CUDA tensor memory)
+ *     owned by the caller; row-major, series-major batches; ld = elements between
+ *     consecutive series (>= n);
+ *   - complex outputs are interleaved float32 pairs (re, im);
+ *   - work is enqueued on `stream` (a hipStream_t; NULL = default stream) and the
+ *     call returns without synchronising; no allocation happens inside a call, so
+ *     calls can be captured into a hipGraph;
+ *   - return value: 0 success, -1 invalid argument, -2 unsupported size,
+ *     > 0 a hipError_t from the kernel launch;
+ *   - calls are stateless and thread-safe.
+ */
+#ifndef WTMI_H
+#define WTMI_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- CWT (K1+K2) --------------------------------------------------------------
+ * Replaces pycwt.cwt(signal, dt, dj, s0, J, Morlet(f0)) as called from
+ * src/cwt.py:110-112 (power |W|^2 at :114, significance ratio at :123-133).
+ * x: [batch][ld] float32, n0 <= 16384 samples used per series.
+ * affine: optional [batch][3] float64 (a0, a1, a2): x' = (x - a0 - a1*t) * a2 applied
+ *         before the transform (standardize_series / pycwt normalisation), or NULL.
+ * scales: [n_scales] float64 (s_j).  sig_scale: [n_scales] float64 = 1/signif_j, or
+ *         NULL when out_sig is NULL.
+ * Outputs (any may be NULL, not all): out_w [batch][n_scales][n0] complex64,
+ *         out_power / out_sig [batch][n_scales][n0] float32.                       */
+int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
+                    const double* affine, const double* scales, int n_scales, double dt,
+                    double f0, const double* sig_scale, float* out_w, float* out_power,
+                    float* out_sig, void* stream);
+
+/* ---- XWT / phase (K1+K2, pair mode) ------------------------------------------
+ * Replaces the two pycwt.cwt calls and W1*conj(W2) inside pycwt.xwt
+ * (src/xwt.py:93-101) and the phase angle(W12) of pycwt.wct used for the arrows
+ * (src/xwt.py:122-137, src/wct.py:106-138).  Outputs: W12 complex64, |W12|^2,
+ * |W12|^2 * sig_scale_j, and the arrow components u = cos(pi/2 - angle(W12)),
+ * v = sin(pi/2 - angle(W12)) (calculate_phase_difference, src/xwt.py:142-154).   */
+int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long batch,
+                    long long n0, const double* affine1, const double* affine2,
+                    const double* scales, int n_scales, double dt, double f0,
+                    const double* sig_scale, float* out_w12, float* out_power, float* out_sig,
+                    float* out_u, float* out_v, void* stream);
+
+/* ---- WCT coherence (K1+K2+K7+K8) ---------------------------------------------
+ * Replaces pycwt.wct(..., sig=False) numerics (src/wct.py:106-118): two CWTs,
+ * Morlet.smooth of |W1|^2/s, |W2|^2/s, W12/s (time Gaussian via FFT + scale boxcar of
+ * `boxcar` rows), WCT = |S12|^2/(S1 S2) and the phase arrows of angle(W12).
+ * workspace: device scratch of wtmi_wct_workspace_bytes(batch, n0, n_scales) bytes.
+ * Outputs (out_u/out_v may be NULL): coherence, u, v [batch][n_scales][n0] float32. */
+long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales);
+int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch, long long n0,
+                    const double* affine1, const double* affine2, const double* scales,
+                    int n_scales, double dt, double f0, int boxcar, void* workspace,
+                    float* out_coh, float* out_u, float* out_v, void* stream);
+
+/* ---- MODWT (K3 / K4) -----------------------------------------------------------
+ * Replace src/modwt.py:126-144 (modwt: rows [W_1..W_J, V_J]) and :147-160 (imodwt).
+ * dec_lo/dec_hi: HOST pointers to the n_taps analysis filters (pywt dec_lo/dec_hi);
+ * the kernels use h~ = dec_hi/sqrt2, g~ = dec_lo/sqrt2 (n_taps <= 128).
+ * w: [batch][level+1][n] float32.  keep_mask (imodwt): bit r set = row r used, others
+ * treated as zero (modwtmra / smooth_signal, src/modwt.py:163-251); ~0ull = all.    */
+int wtmi_modwt(const float* x, long long ld, long long batch, long long n, const double* dec_lo,
+               const double* dec_hi, int n_taps, int level, float* w, void* stream);
+int wtmi_imodwt(const float* w, long long batch, long long n, const double* dec_lo,
+                const double* dec_hi, int n_taps, int level, unsigned long long keep_mask,
+                float* x, long long ld_out, void* stream);
+
+/* ---- DWT (K5 / K6) -------------------------------------------------------------
+ * Replace pywt.wavedec / pywt.waverec with mode "symmetric" (src/dwt.py:104,120;
+ * src/utils/transform_helpers.py:96).  Coefficients of one series are stored
+ * back-to-back in pywt list order [cA_J, cD_J, ..., cD_1]; wtmi_dwt_lengths() gives
+ * the per-array lengths (host, lens[level+1]) and returns the total per series.
+ * waverec: n_variants reconstructions per series, variant v keeps array k when bit k
+ * of keep_masks[v] is set (ResultsFromDWT.smooth_signal, reconstruct_signal_component,
+ * src/dwt.py:53-73,110-120); out: [batch][n_variants][out_len].                   */
+long long wtmi_dwt_lengths(long long n, int n_taps, int level, long long* lens);
+int wtmi_wavedec(const float* x, long long ld, long long batch, long long n, const double* dec_lo,
+                 const double* dec_hi, int n_taps, int level, float* coeffs, void* stream);
+int wtmi_waverec(const float* coeffs, long long batch, long long n, const double* rec_lo,
+                 const double* rec_hi, int n_taps, int level,
+                 const unsigned long long* keep_masks, int n_variants, float* out,
+                 long long out_len, void* stream);
+
+/* ---- per-series moments / affine (K9) -----------------------------------------
+ * Replace standardize_series (src/utils/wavelet_helpers.py:22-57) and the
+ * covariances of pycwt.ar1 (src/cwt.py:106).  out: [batch][8] float64 =
+ * mean, std (ddof 0), slope, intercept, c0, c1, n, 0.                              */
+int wtmi_series_moments(const void* x, int x_is_f64, long long ld, long long batch, long long n,
+                        double* out, void* stream);
+int wtmi_affine(const void* x, int x_is_f64, long long ld_in, long long batch, long long n,
+                const double* coef, void* y, int y_is_f64, long long ld_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WTMI_H */

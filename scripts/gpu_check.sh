@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU session: smoke -> parity tests -> bench -> rocprof kernel trace.
+# Each GPU step has its own time limit; a crash/abort/timeout (exit >= 124 or a
+# signal) ends the session; ordinary test failures (pytest exit 1) do not.
+set -u
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name" ; date
+  timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -5 $OUT/$name.log
+  if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "FATAL in $name (rc=$rc): stopping"; exit $rc; fi
+  return $rc
+}
+STEPS=${STEPS:-"smoke tests bench prof"}
+for s in $STEPS; do
+  case $s in
+    smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    tests) step pytest_gpu 1500 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} ; [ $? -le 1 ] || exit 1 ;;
+    bench) step bench 600 python bench.py ${BENCH_ARGS:-} || exit $? ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} || exit $? ;;
+  esac
+done
+echo ALLDONE

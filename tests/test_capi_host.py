@@ -1,0 +1,115 @@
+"""CPU-side checks: the C ABI library loads and exports what include/wtmi.h declares,
+argument validation fails loudly without touching a GPU, and the host-side closed
+forms of the engine match the oracle."""
+
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "wtmi.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(wtmi_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from wtmi import _lib
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 11
+    for n in names:
+        assert hasattr(lib, n), n
+    assert sorted(_lib.PROTOTYPES) == names
+
+
+def test_prototype_arity_matches_header():
+    from wtmi import _lib
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for name, (_, args) in _lib.PROTOTYPES.items():
+        m = re.search(name + r"\s*\(([^;]*)\)\s*;", txt, flags=re.S)
+        assert m, name
+        nargs = len([a for a in m.group(1).split(",") if a.strip()])
+        assert nargs == len(args), (name, nargs, len(args))
+
+
+def test_invalid_arguments_rejected_without_gpu():
+    from wtmi import _lib
+    lib = _lib.load()
+    assert lib.wtmi_cwt_morlet(None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, None, None, None,
+                               None) == -1
+    assert lib.wtmi_modwt(None, 16, 1, 16, None, None, 8, 2, None, None) == -1
+    assert lib.wtmi_wavedec(None, 16, 1, 16, None, None, 8, 2, None, None) == -1
+    assert lib.wtmi_series_moments(None, 0, 1, 1, 1, None, None) == -1
+    with pytest.raises(_lib.WtmiError, match="invalid argument"):
+        _lib.call("wtmi_affine", None, 0, 1, 1, 1, None, None, 0, 1, None)
+
+
+def test_dwt_lengths_match_pywt_convention(dwt_golden):
+    from wtmi import ops
+    from oracle import dwt_spec as ds
+    g = dwt_golden
+    for i in range(int(g["ncases"])):
+        nlev = int(g[f"c{i}_nlev"])
+        x = g[f"c{i}_x"]
+        lens = [g[f"c{i}_coef{k}"].size for k in range(nlev)]
+        F = {"db4": 8, "db2": 4, "haar": 2, "sym5": 10}[str(g[f"c{i}_wavelet"])]
+        assert ops.dwt_lengths(x.size, F, nlev - 1) == lens
+        assert ds.dwt_max_level(x.size, F) == int(g[f"c{i}_maxlevel"])
+
+
+def test_wavelet_banks_match_pywt(pywt_filters):
+    from wtmi.wavelets import Wavelet, as_filter_bank, wavelist
+    assert "db4" in wavelist()
+    for name, f in pywt_filters.items():
+        w = Wavelet(name)
+        for k in ("dec_lo", "dec_hi", "rec_lo", "rec_hi"):
+            np.testing.assert_array_equal(getattr(w, k), np.asarray(f[k]), err_msg=(name, k))
+    assert as_filter_bank("db4").dec_len == 8
+    with pytest.raises(ValueError):
+        Wavelet("nope")
+
+
+def test_host_closed_forms_match_oracle():
+    from oracle import pycwt_spec as pc
+    from wtmi import transforms as T
+    from wtmi.wavelets import Morlet
+    m = Morlet(6)
+    for n0, dj, J in ((1333, 1 / 12, 84), (8192, 1 / 8, -1), (100, 1 / 4, -1)):
+        sj, fr = T.scales_for(n0, 1 / 12, dj, 2 / 12, J, m)
+        rsj, rfr = pc.scales_for(n0, 1 / 12, dj, 2 / 12, J, pc.Morlet(6))
+        np.testing.assert_array_equal(sj, rsj)
+        np.testing.assert_array_equal(fr, rfr)
+        W, rsj2, rfr2, coi, _, _ = pc.cwt(np.ones(n0), 1 / 12, dj, 2 / 12, J)
+        np.testing.assert_allclose(T.cone_of_influence(n0, 1 / 12, m), coi, rtol=1e-15)
+    sj = (1 / 6) * 2 ** (np.arange(20) / 12)
+    np.testing.assert_allclose(T.significance(1.0, 1 / 12, sj, 0, 0.72)[0],
+                               pc.significance(1.0, 1 / 12, sj, 0, 0.72)[0], rtol=1e-12)
+    assert np.isclose(T.chi2_ppf_dof2(0.95), 5.991464547107979)
+    assert T.boxcar_rows(m, 1 / 8) == 10 and T.boxcar_rows(m, 1 / 12) == 14
+    # AR(1) closed form from covariances == pycwt ar1
+    rng = np.random.default_rng(0)
+    e = rng.standard_normal(500)
+    x = np.zeros(500)
+    for i in range(1, 500):
+        x[i] = 0.5 * x[i - 1] + e[i]
+    xc = x - x.mean()
+    g = T._ar1_from_moments(xc @ xc / x.size, xc[:-1] @ xc[1:] / (x.size - 1), x.size)
+    np.testing.assert_allclose(g, pc.ar1(x), rtol=1e-12)
+
+
+def test_gpu_entry_points_fail_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from wtmi import transforms
+    with pytest.raises(RuntimeError, match="GPU"):
+        transforms.standardize_series(np.arange(10.0))
+    from wtmi import ops
+    with pytest.raises(RuntimeError, match="GPU"):
+        ops.cwt_morlet(torch.zeros(2, 32), [1.0], 1.0)

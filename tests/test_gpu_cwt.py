@@ -1,0 +1,116 @@
+"""CWT / XWT kernel parity vs the fp64 oracle (pycwt restatement).
+
+Tolerance: per (series, scale) row ||W - W_ref|| / ||W_ref|| <= 1e-5.
+Parity is against the restated pycwt algorithm (pycwt itself is absent: "parity
+unpinned", pinned by tests/test_oracle_cwt.py known answers).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import red_series, row_relerr
+from oracle import pycwt_spec as pc
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _ops():
+    from wtmi import ops
+    return ops
+
+
+def _scales(n0, dt, dj, s0, J):
+    return s0 * 2 ** (np.arange(J + 1) * dj)
+
+
+@pytest.mark.parametrize("n0,dj,J", [(5, 1 / 4, 6), (8, 1 / 4, 8), (16, 1 / 4, 12),
+                                     (37, 1 / 8, 30), (100, 1 / 8, 40), (256, 1 / 8, 50),
+                                     (1000, 1 / 12, 70), (1333, 1 / 12, 84), (2048, 1 / 12, 90),
+                                     (4096, 1 / 12, 127), (8192, 1 / 8, 96), (16384, 1 / 4, 50)])
+def test_cwt_rows_match_oracle(n0, dj, J):
+    rng = np.random.default_rng(n0)
+    B = 3
+    x = np.stack([red_series(rng, n0) for _ in range(B)])
+    dt, s0 = 1 / 12, 2 / 12
+    sj = _scales(n0, dt, dj, s0, J)
+    xd = torch.tensor(x, device="cuda")
+    ss = 1.0 / (1.0 + np.arange(sj.size))
+    r = _ops().cwt_morlet(xd, sj, dt, 6.0, sig_scale=ss, want_w=True, want_power=True,
+                          want_sig=True)
+    torch.cuda.synchronize()
+    W = r["w"].cpu().numpy()
+    P = r["power"].cpu().numpy()
+    Sg = r["sig"].cpu().numpy()
+    assert W.shape == (B, sj.size, n0) and W.dtype == np.complex64
+    for b in range(B):
+        ref = pc.cwt(x[b].astype(np.float64), dt, dj, s0, J)[0]
+        err = row_relerr(W[b].astype(np.complex128), ref)
+        assert err.max() < TOL, (b, err.max(), int(err.argmax()))
+        perr = row_relerr(P[b].astype(np.float64), np.abs(ref) ** 2)
+        assert perr.max() < 2 * TOL
+    np.testing.assert_allclose(Sg, P * ss[None, :, None], rtol=1e-6)
+
+
+def test_many_scales_span_several_chunks():
+    rng = np.random.default_rng(99)
+    n0, dt, dj, s0, J = 300, 1 / 12, 1 / 64, 2 / 12, 600  # S = 601 > 512-row chunk table
+    x = red_series(rng, n0)
+    sj = _scales(n0, dt, dj, s0, J)
+    W = _ops().cwt_morlet(torch.tensor(x, device="cuda"), sj, dt)["w"][0].cpu().numpy()
+    ref = pc.cwt(x.astype(np.float64), dt, dj, s0, J)[0]
+    assert row_relerr(W.astype(np.complex128), ref).max() < TOL
+
+
+def test_affine_preprocessing_fused_in_load():
+    rng = np.random.default_rng(5)
+    n0, dt = 700, 1 / 12
+    x = (red_series(rng, n0) + 40.0 + 0.05 * np.arange(n0)).astype(np.float32)
+    a0, a1, a2 = 39.0, 0.05, 1 / 3.0
+    sj = _scales(n0, dt, 1 / 12, 2 * dt, 60)
+    aff = torch.tensor([[a0, a1, a2]], dtype=torch.float64, device="cuda")
+    W = _ops().cwt_morlet(torch.tensor(x, device="cuda"), sj, dt, affine=aff)["w"][0].cpu().numpy()
+    xs = ((x.astype(np.float64) - a0 - a1 * np.arange(n0)) * a2).astype(np.float32)
+    ref = pc.cwt(xs.astype(np.float64), dt, 1 / 12, 2 * dt, 60)[0]
+    assert row_relerr(W.astype(np.complex128), ref).max() < TOL
+
+
+@pytest.mark.parametrize("n0", [64, 1333, 4096])
+def test_xwt_pair_outputs(n0):
+    rng = np.random.default_rng(n0 + 1)
+    B = 2
+    y1 = np.stack([red_series(rng, n0) for _ in range(B)])
+    y2 = (0.6 * np.roll(y1, 3, axis=1) + 0.8 * np.stack([red_series(rng, n0) for _ in range(B)])
+          ).astype(np.float32)
+    dt, dj, s0 = 1 / 12, 1 / 8, 2 / 12
+    J = int(np.round(np.log2(n0 * dt / s0) / dj))
+    sj = _scales(n0, dt, dj, s0, J)
+    ss = np.linspace(0.5, 2.0, sj.size)
+    r = _ops().xwt_morlet(torch.tensor(y1, device="cuda"), torch.tensor(y2, device="cuda"), sj, dt,
+                          sig_scale=ss, want_w12=True, want_power=True, want_sig=True,
+                          want_uv=True)
+    torch.cuda.synchronize()
+    for b in range(B):
+        W1 = pc.cwt(y1[b].astype(np.float64), dt, dj, s0, J)[0]
+        W2 = pc.cwt(y2[b].astype(np.float64), dt, dj, s0, J)[0]
+        W12 = W1 * W2.conj()
+        g = r["w12"][b].cpu().numpy().astype(np.complex128)
+        assert row_relerr(g, W12).max() < 2 * TOL
+        p = r["power"][b].cpu().numpy().astype(np.float64)
+        assert row_relerr(p, np.abs(W12) ** 2).max() < 4 * TOL
+        ang = np.angle(W12)
+        u, v = r["u"][b].cpu().numpy(), r["v"][b].cpu().numpy()
+        mask = np.abs(W12) > 1e-3 * np.abs(W12).max()
+        np.testing.assert_allclose(u[mask], np.cos(0.5 * np.pi - ang)[mask], atol=1e-4)
+        np.testing.assert_allclose(v[mask], np.sin(0.5 * np.pi - ang)[mask], atol=1e-4)
+
+
+def test_rejects_cpu_tensors_and_bad_args():
+    ops = _ops()
+    with pytest.raises(RuntimeError):
+        ops.cwt_morlet(torch.zeros(1, 16), [1.0], 1.0)
+    from wtmi import _lib
+    with pytest.raises(_lib.WtmiError):
+        _lib.call("wtmi_cwt_morlet", None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, None, None,
+                  None, None)

@@ -1,0 +1,190 @@
+"""WCT kernels, per-series moments and the drop-in src.* modules vs the oracle.
+
+WCT tolerance: coherence elementwise abs <= 1e-4; phase arrows compared
+where |W12| > 1e-3 max.  The drop-in modules are compared with the oracle's
+restatement of the reference wrapper glue (oracle/glue_spec.py).
+"""
+
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from gpu_helpers import red_series, row_relerr
+from oracle import glue_spec as gs
+from oracle import pycwt_spec as pc
+
+pytestmark = pytest.mark.gpu
+SAMPLE = os.path.join(os.path.dirname(__file__), "golden", "sample_data")
+
+
+def load_sample(name):
+    df = pd.read_csv(os.path.join(SAMPLE, name), sep=None, parse_dates=[0], index_col=0,
+                     engine="python")
+    return df.iloc[:, 0].to_numpy(dtype=float), df.index.to_numpy()
+
+
+def _pair(rng, n):
+    y1 = red_series(rng, n).astype(np.float64)
+    y2 = 0.6 * np.roll(y1, 3) + 0.8 * red_series(rng, n)
+    return y1, y2
+
+
+@pytest.mark.parametrize("n,dj", [(64, 1 / 8), (256, 1 / 8), (1000, 1 / 8), (1333, 1 / 12),
+                                  (2048, 1 / 8), (8192, 1 / 8)])
+def test_wct_matches_oracle(n, dj):
+    from wtmi import transforms
+    rng = np.random.default_rng(n)
+    y1, y2 = _pair(rng, n)
+    coh, aw, coi, freq, sig = transforms.wct(y1, y2, 1 / 12, dj=dj, s0=2 / 12, J=-1, sig=False)
+    rc, ra, rcoi, rfreq, rsig = pc.wct(y1, y2, 1 / 12, dj=dj, s0=2 / 12, J=-1, sig=False)
+    assert coh.shape == rc.shape
+    assert np.abs(coh - rc).max() <= 1e-4, np.abs(coh - rc).max()
+    W12 = (pc.cwt((y1 - y1.mean()) / y1.std(), 1 / 12, dj, 2 / 12, -1)[0]
+           * pc.cwt((y2 - y2.mean()) / y2.std(), 1 / 12, dj, 2 / 12, -1)[0].conj())
+    mask = np.abs(W12) > 1e-3 * np.abs(W12).max()
+    dphi = np.angle(np.exp(1j * (aw - ra)))
+    assert np.abs(dphi[mask]).max() <= 1e-4
+    np.testing.assert_allclose(coi, rcoi, rtol=1e-12)
+    np.testing.assert_allclose(freq, rfreq, rtol=1e-12)
+
+
+def test_wct_batched_self_coherence_is_one():
+    from wtmi import transforms
+    rng = np.random.default_rng(2)
+    B, n = 8, 512
+    y = torch.tensor(np.stack([red_series(rng, n) for _ in range(B)]), device="cuda")
+    res, sj, _ = transforms.wct_batch(y, y, 1 / 12, 1 / 8, 2 / 12, -1)
+    c = res["coh"].cpu().numpy()
+    assert np.abs(c - 1).max() < 1e-4
+
+
+def test_moments_and_standardize_match_numpy():
+    from wtmi import ops, transforms
+    rng = np.random.default_rng(4)
+    for n in (2, 17, 1333, 5000):
+        x = rng.standard_normal(n).cumsum() + 100
+        m = ops.series_moments(torch.tensor(x, device="cuda")).cpu().numpy()[0]
+        p = np.polyfit(np.arange(n), x, 1)
+        xc = x - x.mean()
+        np.testing.assert_allclose(m[:4], [x.mean(), x.std(), p[0], p[1]], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(m[4], xc @ xc / n, rtol=1e-10)
+        np.testing.assert_allclose(m[5], xc[:-1] @ xc[1:] / (n - 1), rtol=1e-10, atol=1e-12)
+        for kw in (dict(), dict(detrend=False, remove_mean=True), dict(detrend=False),
+                   dict(standardize=False)):
+            np.testing.assert_allclose(transforms.standardize_series(x, **kw),
+                                       gs.standardize_series(x, **kw), rtol=1e-9, atol=1e-9)
+    with pytest.raises(ValueError):
+        transforms.standardize_series(x, detrend=True, remove_mean=True)
+
+
+def test_ar1_and_cpi_fallback_warning():
+    from wtmi import transforms
+    y, _ = load_sample("inflation.csv")
+    ys = gs.standardize_series(y)
+    g, a, mu2 = transforms.ar1(ys)
+    rg, ra, rmu = pc.ar1(ys)
+    np.testing.assert_allclose([g, a, mu2], [rg, ra, rmu], rtol=1e-9)
+    cpi, _ = load_sample("cpi.csv")
+    with pytest.raises(Warning):
+        transforms.ar1(gs.standardize_series(cpi))
+
+
+def test_src_cwt_run_cwt_on_inflation():
+    import src.cwt as cwt
+    from src.utils.wavelet_helpers import standardize_series
+    y, t = load_sample("inflation.csv")
+    ys = standardize_series(y)  # the app standardises before run_cwt (quirk B.2)
+    data = cwt.DataForCWT(t, ys, cwt.MOTHER, cwt.DT, cwt.DJ, cwt.S0, cwt.LEVELS)
+    assert data.time_range.shape == (y.size,)
+    for kwargs in (dict(), dict(standardize=True), dict(calculate_significance=False)):
+        res = cwt.run_cwt(data, **kwargs)
+        p, period, sig, coi = gs.run_cwt(
+            ys, y.size, standardize=kwargs.get("standardize", False),
+            calculate_significance=kwargs.get("calculate_significance", True))
+        assert res.power.shape == p.shape == (85, 1333)
+        assert row_relerr(res.power, p).max() < 2e-5
+        np.testing.assert_allclose(res.period, period, rtol=1e-12)
+        np.testing.assert_allclose(res.coi, coi, rtol=1e-12)
+        if sig is None:
+            assert res.significance_levels is None
+        else:
+            assert row_relerr(res.significance_levels, sig).max() < 2e-5
+
+
+def test_src_cwt_64_scales_config1():
+    """BASELINE config 1: inflation.csv, 64 scales (J = 63)."""
+    from wtmi import ops, transforms
+    y, _ = load_sample("inflation.csv")
+    ys = gs.standardize_series(y)
+    sj, freqs = transforms.scales_for(y.size, 1 / 12, 1 / 12, 2 / 12, 63, transforms.as_morlet(None))
+    assert sj.size == 64
+    P = ops.cwt_morlet(torch.tensor(ys, device="cuda", dtype=torch.float32), sj, 1 / 12,
+                       want_w=False, want_power=True)["power"][0].cpu().numpy()
+    ref = np.abs(pc.cwt(ys.astype(np.float32).astype(np.float64), 1 / 12, 1 / 12, 2 / 12, 63)[0]) ** 2
+    assert row_relerr(P.astype(np.float64), ref).max() < 2e-5
+
+
+def test_src_xwt_and_wct():
+    import src.wct as wct
+    import src.xwt as xwt
+    rng = np.random.default_rng(12)
+    y1, y2 = _pair(rng, 600)
+    d = xwt.DataForXWT(y1, y2, xwt.MOTHER_DICT["morlet"], xwt.DT, xwt.DJ, xwt.S0, xwt.LEVELS)
+    r = xwt.run_xwt(d)
+    ref = gs.run_xwt(y1, y2, xwt.DT, xwt.DJ, xwt.S0, xwt.LEVELS)
+    assert r.power.shape == ref[0].shape
+    assert row_relerr(r.power, ref[0]).max() < 5e-5
+    np.testing.assert_allclose(r.period, ref[1], rtol=1e-12)
+    assert row_relerr(r.significance_levels, ref[2]).max() < 5e-5
+    np.testing.assert_allclose(r.coi, ref[3], rtol=1e-12)
+    assert r.phase_diff_u.shape == ref[4].shape  # phase at dj = 1/12 (quirk B.5)
+    assert r.phase_diff_u.shape[0] != r.power.shape[0]
+    W12 = (pc.cwt((y1 - y1.mean()) / y1.std(), 1 / 12, 1 / 12, xwt.S0, -1)[0]
+           * pc.cwt((y2 - y2.mean()) / y2.std(), 1 / 12, 1 / 12, xwt.S0, -1)[0].conj())
+    mask = np.abs(W12) > 1e-3 * np.abs(W12).max()
+    np.testing.assert_allclose(r.phase_diff_u[mask], ref[4][mask], atol=1e-4)
+    np.testing.assert_allclose(r.phase_diff_v[mask], ref[5][mask], atol=1e-4)
+
+    dw = wct.DataForWCT(y1, y2, wct.MOTHER_DICT["morlet"], wct.DT, wct.DJ, wct.S0, wct.LEVELS)
+    rw = wct.run_wct(dw, calculate_signficance=False)
+    refw = gs.run_wct(y1, y2, wct.DT, wct.DJ, wct.S0)
+    assert np.abs(rw.coherence - refw[0]).max() <= 1e-4
+    assert np.isinf(rw.significance_levels).all() and np.isinf(refw[2]).all()  # quirk B.8
+    with pytest.raises(NotImplementedError):
+        wct.run_wct(dw, calculate_signficance=True)
+
+
+def test_src_dwt_and_modwt(dwt_golden, modwt_golden):
+    import src.dwt as dwt
+    import src.modwt as modwt
+    g = dwt_golden
+    for i in range(int(g["ncases"])):
+        if f"c{i}_comp0" not in g:
+            continue
+        x = g[f"c{i}_x"]
+        nlev = int(g[f"c{i}_nlev"])
+        lvl0 = int(g[f"c{i}_level"])
+        res = dwt.run_dwt(dwt.DataForDWT(x, dwt.MOTHER, None if lvl0 < 0 else lvl0))
+        assert res.levels == nlev - 1
+        for k, c in enumerate(res.coeffs):
+            ref = g[f"c{i}_coef{k}"]
+            assert c.shape == ref.shape and np.abs(c - ref).max() <= 1e-5 * np.abs(ref).max()
+        res.smooth_signal(x, dwt.MOTHER)
+        for lvl, dd in res.smoothed_signal_dict.items():
+            ref = g[f"c{i}_smooth{lvl}"]
+            assert np.abs(dd["signal"] - ref).max() <= 1e-5 * np.abs(ref).max()
+        comp = dwt.reconstruct_signal_component(res.coeffs, dwt.MOTHER, 1)
+        ref = g[f"c{i}_comp1"]
+        assert np.abs(comp - ref).max() <= 1e-5 * max(np.abs(ref).max(), 1e-12)
+    m = modwt_golden
+    for i in range(int(m["ncases"])):
+        x, w, J = m[f"c{i}_x"], m[f"c{i}_w"], int(m[f"c{i}_J"])
+        got = modwt.modwt(x, "db4", J)
+        assert got.dtype == x.dtype and got.shape == w.shape
+        assert np.abs(got - w).max() <= 1e-5 * np.abs(w).max()
+        if f"c{i}_mra" in m:
+            mra = modwt.modwtmra(w, "db4")
+            assert np.abs(mra - m[f"c{i}_mra"]).max() <= 1e-5 * np.abs(w).max()

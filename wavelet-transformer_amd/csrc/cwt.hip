@@ -1,0 +1,300 @@
+// Fused Morlet CWT / cross-wavelet kernels (K1 + K2 of DESIGN.md).
+//
+// Replaces pycwt.cwt as called from src/cwt.py:110 (and the two cwt calls inside
+// pycwt.xwt, src/xwt.py:93): N = 2^ceil(log2 n0); X = FFT(x zero-padded to N);
+// W_j = IFFT(X * sqrt(2 pi s_j / dt) * pi^-1/4 * exp(-(s_j w_k - f0)^2 / 2))[:n0].
+//
+// One workgroup = one series (or pair) x a chunk of scales.  The forward FFT runs
+// once per workgroup and the spectrum stays in registers (16 complex per thread);
+// each scale row is an analytic-filter multiply + in-LDS inverse FFT + a fused
+// epilogue writing any of {W (complex64), |W|^2, |W|^2 / signif_j} (cross mode:
+// {W1 W2*, |W1 W2*|^2, ratio, phase arrows u = sin(angle), v = cos(angle)}).
+// The Morlet filter is evaluated in-register: no filter bank is read from HBM.
+#include "cwt_common.hpp"
+
+namespace wtmi {
+
+enum : int { kOutW = 1, kOutPow = 2, kOutSig = 4, kOutUV = 8 };
+
+template <int LOGN, int KIND, bool FULL>
+__device__ __forceinline__ void store_row(const float2 (&v)[16], const CwtArgs& a, long long rowbase,
+                                          float sg, int t) {
+  using P = FftPlan<LOGN>;
+  float2* pw_ = (KIND & kOutW) ? a.out_w + rowbase : nullptr;
+  float* pp_ = (KIND & kOutPow) ? a.out_pow + rowbase : nullptr;
+  float* ps_ = (KIND & kOutSig) ? a.out_sig + rowbase : nullptr;
+  float* pu_ = (KIND & kOutUV) ? a.out_u + rowbase : nullptr;
+  float* pv_ = (KIND & kOutUV) ? a.out_v + rowbase : nullptr;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int pos = t + m * P::NT;
+    if (FULL || pos < a.n0) {
+      if constexpr (KIND & kOutW) pw_[pos] = v[m];
+      const float pw = cabs2(v[m]);
+      if constexpr (KIND & kOutPow) pp_[pos] = pw;
+      if constexpr (KIND & kOutSig) ps_[pos] = pw * sg;
+      if constexpr (KIND & kOutUV) {
+        const float r = sqrtf(pw);
+        pu_[pos] = r > 0.f ? v[m].y / r : 0.f;
+        pv_[pos] = r > 0.f ? v[m].x / r : 1.f;
+      }
+    }
+  }
+}
+
+template <int LOGN, bool FULL>
+__device__ __forceinline__ void store_any(const float2 (&v)[16], const CwtArgs& a, int kind,
+                                          long long rowbase, float sg, int t) {
+  switch (kind) {
+#define WTMI_K(K) case K: store_row<LOGN, K, FULL>(v, a, rowbase, sg, t); break;
+    WTMI_K(1) WTMI_K(2) WTMI_K(3) WTMI_K(4) WTMI_K(5) WTMI_K(6) WTMI_K(7) WTMI_K(8)
+    WTMI_K(9) WTMI_K(10) WTMI_K(11) WTMI_K(12) WTMI_K(13) WTMI_K(14) WTMI_K(15)
+#undef WTMI_K
+    default: break;
+  }
+}
+
+constexpr int kMaxChunk = 512;  // per-workgroup scale-parameter table in LDS
+
+template <int LOGN, int NBUF, int MODE>
+__global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 : CwtGeom<LOGN, MODE>::MINW)) cwt_morlet_kernel(CwtArgs a) {
+  using P = FftPlan<LOGN>;
+  using G = CwtGeom<LOGN, MODE>;
+  __shared__ float2 lds[NBUF * G::ROWS * P::PADN + kMaxChunk];
+  float2* prm_tab = lds + NBUF * G::ROWS * P::PADN;
+  const int tid = threadIdx.x;
+  const int g = tid / P::NT;
+  const int t = tid - g * P::NT;
+  const long long blk = blockIdx.x;
+  const long long b = blk / a.nchunks;
+  const int ch = static_cast<int>(blk - b * a.nchunks);
+  const int j0 = ch * a.chunk;
+  const int j1 = min(a.S, j0 + a.chunk);
+  float2* my = lds + g * P::PADN;
+  constexpr int bufstride = G::ROWS * P::PADN;
+
+  for (int i = tid; i < j1 - j0; i += G::BLOCK) prm_tab[i] = morlet_params(a.scales[j0 + i], a.dt, P::N);
+
+  float2 tw[P::NTW_ALLOC];
+  fft_twiddles<LOGN>(tw, t);
+  int par = 0;
+
+  float2 X[16];
+  load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
+  fft_row<LOGN, -1, NBUF>(X, my, bufstride, tw, t, par);
+  float2 X2[MODE == 1 ? 16 : 1];
+  if constexpr (MODE == 1) {
+    load_series<LOGN>(X2, a.x2, a.affine2, b, a.ld, a.n0, t);
+    fft_row<LOGN, -1, NBUF>(X2, my, bufstride, tw, t, par);
+  }
+  __syncthreads();  // prm_tab visible (the FFT barriers may be absent for N = 16)
+
+  const int kind = (a.out_w ? kOutW : 0) | (a.out_pow ? kOutPow : 0) | (a.out_sig ? kOutSig : 0) |
+                   (a.out_u ? kOutUV : 0);
+  const bool full = a.n0 == P::N;
+  const float f0 = static_cast<float>(a.f0);
+  const int iters = (j1 - j0 + G::ROWS - 1) / G::ROWS;
+  for (int it = 0; it < iters; ++it) {
+    const int jl = it * G::ROWS + g;
+    const bool valid = jl < j1 - j0;
+    const float2 prm = prm_tab[valid ? jl : 0];
+    float2 v[16];
+    morlet_filter<LOGN>(v, X, prm, f0, t);
+    fft_row<LOGN, 1, NBUF>(v, my, bufstride, tw, t, par);
+    if constexpr (MODE == 1) {
+      float2 w1[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) w1[m] = v[m];
+      morlet_filter<LOGN>(v, X2, prm, f0, t);
+      fft_row<LOGN, 1, NBUF>(v, my, bufstride, tw, t, par);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = cmul(w1[m], cconj(v[m]));
+    }
+    if (!valid) continue;
+    const int j = j0 + jl;
+    const long long rowbase = (b * a.S + j) * static_cast<long long>(a.n0);
+    const float sg = a.sigscale ? static_cast<float>(a.sigscale[j]) : 0.f;
+    if (full)
+      store_any<LOGN, true>(v, a, kind, rowbase, sg, t);
+    else
+      store_any<LOGN, false>(v, a, kind, rowbase, sg, t);
+  }
+}
+
+// Direct-DFT path for N < 16 (n0 <= 8): one thread per output sample.
+template <int MODE>
+__global__ void __launch_bounds__(256) cwt_direct_kernel(CwtArgs a, int N) {
+  const long long idx = blockIdx.x * 256ll + threadIdx.x;
+  const long long total = a.batch * a.S * a.n0;
+  if (idx >= total) return;
+  const int tpos = static_cast<int>(idx % a.n0);
+  const long long rj = idx / a.n0;
+  const int j = static_cast<int>(rj % a.S);
+  const long long b = rj / a.S;
+  const double s = a.scales[j];
+  const double alpha = s * 2.0 * kPi / (N * a.dt);
+  const double c = sqrt(2.0 * kPi * s / a.dt) * 0.75112554446494248286 / N;
+  double2 w[2] = {make_double2(0, 0), make_double2(0, 0)};
+  for (int which = 0; which < (MODE == 1 ? 2 : 1); ++which) {
+    const float* row = (which ? a.x2 : a.x) + b * a.ld;
+    const double* af = which ? a.affine2 : a.affine;
+    double acc_re = 0, acc_im = 0;
+    for (int k = 0; k < N; ++k) {
+      double xr = 0, xi = 0;  // X[k]
+      for (int n = 0; n < a.n0; ++n) {
+        double val = row[n];
+        if (af) val = static_cast<float>((val - af[3 * b] - af[3 * b + 1] * n) * af[3 * b + 2]);
+        double sn, cs;
+        sincospi(-2.0 * ((static_cast<long long>(k) * n) % N) / N, &sn, &cs);
+        xr += val * cs;
+        xi += val * sn;
+      }
+      const int kk = k < N / 2 ? k : k - N;
+      const double e = alpha * kk - a.f0;
+      const double psi = c * exp(-0.5 * e * e);
+      double sn, cs;
+      sincospi(2.0 * ((static_cast<long long>(k) * tpos) % N) / N, &sn, &cs);
+      acc_re += psi * (xr * cs - xi * sn);
+      acc_im += psi * (xr * sn + xi * cs);
+    }
+    w[which] = make_double2(acc_re, acc_im);
+  }
+  float2 v = make_float2(static_cast<float>(w[0].x), static_cast<float>(w[0].y));
+  if constexpr (MODE == 1) {
+    const float2 w2 = make_float2(static_cast<float>(w[1].x), static_cast<float>(w[1].y));
+    v = cmul(v, cconj(w2));
+  }
+  const long long o = idx;
+  if (a.out_w) a.out_w[o] = v;
+  const float pw = cabs2(v);
+  if (a.out_pow) a.out_pow[o] = pw;
+  if (a.out_sig) a.out_sig[o] = pw * static_cast<float>(a.sigscale[j]);
+  if constexpr (MODE == 1) {
+    if (a.out_u) {
+      const float r = sqrtf(pw);
+      a.out_u[o] = r > 0.f ? v.y / r : 0.f;
+      a.out_v[o] = r > 0.f ? v.x / r : 1.f;
+    }
+  }
+}
+
+static int log2_ceil(long long n) {
+  int l = 0;
+  while ((1ll << l) < n) ++l;
+  return l;
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return s ? atoi(s) : dflt;
+}
+
+template <int LOGN, int NBUF, int MODE>
+static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
+  using G = CwtGeom<LOGN, MODE>;
+  // Scale chunking: enough workgroups to fill 256 CUs several times, while keeping
+  // at least 4 row-iterations per workgroup to amortise the forward FFT.
+  const int rows = G::ROWS;
+  const int target = env_int("WTMI_CWT_TARGET_WG", 4096);
+  long long want = (target + a.batch - 1) / a.batch;
+  const int max_chunks = (a.S + 4 * rows - 1) / (4 * rows);
+  int nch = static_cast<int>(want < 1 ? 1 : want);
+  if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
+  int chunk = (a.S + nch - 1) / nch;
+  chunk = ((chunk + rows - 1) / rows) * rows;
+  if (chunk > kMaxChunk) chunk = kMaxChunk;
+  nch = (a.S + chunk - 1) / chunk;
+  a.nchunks = nch;
+  a.chunk = chunk;
+  const long long grid = a.batch * nch;
+  if (grid > 0x7fffffffll) return kErrUnsupported;
+  hipLaunchKernelGGL((cwt_morlet_kernel<LOGN, NBUF, MODE>), dim3(static_cast<unsigned>(grid)),
+                     dim3(G::BLOCK), 0, st, a);
+  return launch_status();
+}
+
+template <int MODE>
+static int dispatch(CwtArgs& a, hipStream_t st) {
+  if (a.batch == 0 || a.S == 0 || a.n0 == 0) return kOk;
+  const int logn = log2_ceil(a.n0);
+  if (logn < 4) {
+    const int N = 1 << logn;
+    const long long total = a.batch * a.S * a.n0;
+    const long long blocks = (total + 255) / 256;
+    hipLaunchKernelGGL((cwt_direct_kernel<MODE>), dim3(static_cast<unsigned>(blocks)), dim3(256),
+                       0, st, a, N);
+    return launch_status();
+  }
+  const int nbuf = env_int("WTMI_CWT_NBUF", 1);
+#define WTMI_CASE(L)                                                   \
+  case L:                                                              \
+    return nbuf == 2 && L <= 13 ? launch_fft_cwt<L, (L <= 13 ? 2 : 1), MODE>(a, st) \
+                                : launch_fft_cwt<L, 1, MODE>(a, st);
+  switch (logn) {
+    WTMI_CASE(4) WTMI_CASE(5) WTMI_CASE(6) WTMI_CASE(7) WTMI_CASE(8) WTMI_CASE(9)
+    WTMI_CASE(10) WTMI_CASE(11) WTMI_CASE(12) WTMI_CASE(13) WTMI_CASE(14)
+    default:
+      return kErrUnsupported;
+  }
+#undef WTMI_CASE
+}
+
+}  // namespace wtmi
+
+using namespace wtmi;
+
+extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
+                               const double* affine, const double* scales, int n_scales,
+                               double dt, double f0, const double* sig_scale, float* out_w,
+                               float* out_power, float* out_sig, void* stream) {
+  if (!x || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
+  if (!out_w && !out_power && !out_sig) return kErrArg;
+  if (out_sig && !sig_scale) return kErrArg;
+  if (n0 > (1 << 14)) return kErrUnsupported;
+  CwtArgs a{};
+  a.x = x;
+  a.ld = ld;
+  a.batch = batch;
+  a.n0 = static_cast<int>(n0);
+  a.S = n_scales;
+  a.affine = affine;
+  a.scales = scales;
+  a.dt = dt;
+  a.f0 = f0;
+  a.sigscale = sig_scale;
+  a.out_w = reinterpret_cast<float2*>(out_w);
+  a.out_pow = out_power;
+  a.out_sig = out_sig;
+  return dispatch<0>(a, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long batch,
+                               long long n0, const double* affine1, const double* affine2,
+                               const double* scales, int n_scales, double dt, double f0,
+                               const double* sig_scale, float* out_w12, float* out_power,
+                               float* out_sig, float* out_u, float* out_v, void* stream) {
+  if (!x1 || !x2 || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
+  if (!out_w12 && !out_power && !out_sig && !out_u) return kErrArg;
+  if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
+  if (out_sig && !sig_scale) return kErrArg;
+  if (n0 > (1 << 14)) return kErrUnsupported;
+  CwtArgs a{};
+  a.x = x1;
+  a.x2 = x2;
+  a.ld = ld;
+  a.batch = batch;
+  a.n0 = static_cast<int>(n0);
+  a.S = n_scales;
+  a.affine = affine1;
+  a.affine2 = affine2;
+  a.scales = scales;
+  a.dt = dt;
+  a.f0 = f0;
+  a.sigscale = sig_scale;
+  a.out_w = reinterpret_cast<float2*>(out_w12);
+  a.out_pow = out_power;
+  a.out_sig = out_sig;
+  a.out_u = out_u;
+  a.out_v = out_v;
+  return dispatch<1>(a, static_cast<hipStream_t>(stream));
+}

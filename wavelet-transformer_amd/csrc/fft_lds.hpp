@@ -1,0 +1,330 @@
+// Workgroup-cooperative power-of-two FFT held in registers + LDS (gfx950).
+//
+// One row of N = 2^LOGN complex64 samples is spread over NT = N/16 threads; thread
+// t holds the 16 elements at positions t + m*NT (m = 0..15) in registers.  The
+// transform is a Stockham autosort FFT: a radix-16 pass straight from registers,
+// then radix-16 passes and at most one trailing radix-2/4/8 pass, each reading from
+// and writing to LDS (one exchange per pass after the first).  On exit the thread
+// again holds positions t + m*NT, so a caller can keep a spectrum resident in
+// registers across many inverse transforms (the per-scale CWT loop) and stores are
+// coalesced (consecutive lanes -> consecutive samples).
+//
+// LDS rows are padded by one complex per 16 (index i -> i + i/16) so that the
+// radix-16 scatter of pass 0 (lane stride 16 complex) is bank-conflict free for
+// ds_write_b64.  DIR = -1 forward, +1 inverse; the transform is unnormalised.
+#pragma once
+
+#include "common.hpp"
+
+namespace wtmi {
+
+// cos / sin of 2*pi*m/16
+__host__ __device__ constexpr float cos16(int m) {
+  constexpr float c1 = 0.92387953251128674f, c2 = 0.70710678118654752f, c3 = 0.38268343236508977f;
+  switch (m & 15) {
+    case 0: return 1.f;  case 1: return c1;   case 2: return c2;   case 3: return c3;
+    case 4: return 0.f;  case 5: return -c3;  case 6: return -c2;  case 7: return -c1;
+    case 8: return -1.f; case 9: return -c1;  case 10: return -c2; case 11: return -c3;
+    case 12: return 0.f; case 13: return c3;  case 14: return c2;  default: return c1;
+  }
+}
+__host__ __device__ constexpr float sin16(int m) { return cos16(m - 4); }
+
+template <int DIR>
+__device__ __forceinline__ float2 mul_i(float2 a) {  // a * (DIR * i)
+  return DIR > 0 ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+}
+
+template <int DIR, int M>
+__device__ __forceinline__ float2 rot16(float2 a) {  // a * exp(DIR * 2 pi i M / 16)
+  constexpr int m = M & 15;
+  if constexpr (m == 0) {
+    return a;
+  } else if constexpr (m == 4) {
+    return mul_i<DIR>(a);
+  } else if constexpr (m == 8) {
+    return make_float2(-a.x, -a.y);
+  } else if constexpr (m == 12) {
+    return mul_i<-DIR>(a);
+  } else {
+    constexpr float c = cos16(m);
+    constexpr float s = DIR * sin16(m);
+    return make_float2(fmaf(a.x, c, -a.y * s), fmaf(a.x, s, a.y * c));
+  }
+}
+
+template <int DIR>
+__device__ __forceinline__ void dft2(float2& a, float2& b) {
+  const float2 t = a;
+  a = cadd(t, b);
+  b = csub(t, b);
+}
+
+template <int DIR>
+__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
+  const float2 t0 = cadd(x0, x2), t1 = csub(x0, x2);
+  const float2 t2 = cadd(x1, x3), t3 = mul_i<DIR>(csub(x1, x3));
+  x0 = cadd(t0, t2);
+  x2 = csub(t0, t2);
+  x1 = cadd(t1, t3);
+  x3 = csub(t1, t3);
+}
+
+// 8-point DFT on v[0..7], natural order in and out (2 x 4 Cooley-Tukey).
+template <int DIR>
+__device__ __forceinline__ void dft8(float2* v) {
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) dft2<DIR>(v[n2], v[n2 + 4]);
+  v[5] = rot16<DIR, 2>(v[5]);
+  v[6] = rot16<DIR, 4>(v[6]);
+  v[7] = rot16<DIR, 6>(v[7]);
+  dft4<DIR>(v[0], v[1], v[2], v[3]);
+  dft4<DIR>(v[4], v[5], v[6], v[7]);
+  float2 t[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = v[i];
+#pragma unroll
+  for (int k1 = 0; k1 < 2; ++k1)
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) v[k1 + 2 * k2] = t[4 * k1 + k2];
+}
+
+// 16-point DFT on v[0..15], natural order in and out (4 x 4 Cooley-Tukey).
+template <int DIR>
+__device__ __forceinline__ void dft16(float2* v) {
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) dft4<DIR>(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]);
+  v[5] = rot16<DIR, 1>(v[5]);
+  v[9] = rot16<DIR, 2>(v[9]);
+  v[13] = rot16<DIR, 3>(v[13]);
+  v[6] = rot16<DIR, 2>(v[6]);
+  v[10] = rot16<DIR, 4>(v[10]);
+  v[14] = rot16<DIR, 6>(v[14]);
+  v[7] = rot16<DIR, 3>(v[7]);
+  v[11] = rot16<DIR, 6>(v[11]);
+  v[15] = rot16<DIR, 9>(v[15]);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) dft4<DIR>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+  float2 t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = v[i];
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = t[4 * k1 + k2];
+}
+
+template <int R, int DIR>
+__device__ __forceinline__ void dft_small(float2* v) {
+  if constexpr (R == 2) {
+    dft2<DIR>(v[0], v[1]);
+  } else if constexpr (R == 4) {
+    dft4<DIR>(v[0], v[1], v[2], v[3]);
+  } else if constexpr (R == 8) {
+    dft8<DIR>(v);
+  } else {
+    dft16<DIR>(v);
+  }
+}
+
+template <int LOGN>
+struct FftPlan {
+  static_assert(LOGN >= 4 && LOGN <= 14, "FFT length must be 16..16384");
+  static constexpr int N = 1 << LOGN;
+  static constexpr int NT = N / 16;              // threads per row
+  static constexpr int P16 = LOGN / 4;           // radix-16 passes
+  static constexpr int REM = 1 << (LOGN % 4);    // trailing radix (1 = none)
+  static constexpr int NPASS = P16 + (REM > 1 ? 1 : 0);
+  static constexpr int PADN = N + N / 16;        // padded LDS row length (complex)
+  // cached base twiddles per thread: w, w^2, w^4, w^8 per radix-16 pass >= 1,
+  // plus the trailing pass's per-butterfly bases.
+  static constexpr int NTW_REM = REM == 2 ? 8 : (REM == 4 ? 8 : (REM == 8 ? 6 : 0));
+  static constexpr int NTW = (P16 - 1) * 4 + NTW_REM;
+  static constexpr int NTW_ALLOC = NTW > 0 ? NTW : 1;
+};
+
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+
+// exp(+2 pi i num / den), correctly rounded from double.
+__device__ __forceinline__ float2 expi_frac(long long num, long long den) {
+  num %= den;
+  double s, c;
+  sincospi(2.0 * static_cast<double>(num) / static_cast<double>(den), &s, &c);
+  return make_float2(static_cast<float>(c), static_cast<float>(s));
+}
+
+// Per-thread base twiddles (inverse sign; the forward transform conjugates them).
+template <int LOGN>
+__device__ __forceinline__ void fft_twiddles(float2* tw, int t) {
+  using P = FftPlan<LOGN>;
+  long long ns = 16;
+#pragma unroll
+  for (int p = 1; p < P::P16; ++p) {
+    const long long k = t & (ns - 1);
+    const long long M = ns * 16;
+    tw[4 * (p - 1) + 0] = expi_frac(k, M);
+    tw[4 * (p - 1) + 1] = expi_frac(2 * k, M);
+    tw[4 * (p - 1) + 2] = expi_frac(4 * k, M);
+    tw[4 * (p - 1) + 3] = expi_frac(8 * k, M);
+    ns *= 16;
+  }
+  if constexpr (P::REM > 1) {
+    constexpr int base = 4 * (P::P16 - 1);
+    constexpr int R = P::REM;
+#pragma unroll
+    for (int q = 0; q < 16 / R; ++q) {
+      const long long k = t + q * P::NT;
+      if constexpr (R == 2) {
+        tw[base + q] = expi_frac(k, P::N);
+      } else if constexpr (R == 4) {
+        tw[base + 2 * q + 0] = expi_frac(k, P::N);
+        tw[base + 2 * q + 1] = expi_frac(2 * k, P::N);
+      } else {
+        tw[base + 3 * q + 0] = expi_frac(k, P::N);
+        tw[base + 3 * q + 1] = expi_frac(2 * k, P::N);
+        tw[base + 3 * q + 2] = expi_frac(4 * k, P::N);
+      }
+    }
+  }
+}
+
+template <int DIR>
+__device__ __forceinline__ float2 twd(float2 w) { return DIR > 0 ? w : cconj(w); }
+
+// Hide a value from loop-invariant code motion: keeps only the base twiddles live
+// across a caller's loop instead of all 15 derived powers (+ swapped copies for
+// packed math), which otherwise pushes the CWT kernel to 256 VGPRs.
+__device__ __forceinline__ float2 opaque(float2 w) {
+  asm volatile("" : "+v"(w.x), "+v"(w.y));
+  return w;
+}
+
+// v[r] *= w^r for r = 1..15 from the bases w, w^2, w^4, w^8.
+template <int DIR>
+__device__ __forceinline__ void apply_tw16(float2* v, const float2* b) {
+  const float2 w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
+  const float2 w4 = twd<DIR>(opaque(b[2])), w8 = twd<DIR>(opaque(b[3]));
+  const float2 w3 = cmul(w1, w2), w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
+  v[1] = cmul(v[1], w1);
+  v[2] = cmul(v[2], w2);
+  v[3] = cmul(v[3], w3);
+  v[4] = cmul(v[4], w4);
+  v[5] = cmul(v[5], w5);
+  v[6] = cmul(v[6], w6);
+  v[7] = cmul(v[7], w7);
+  v[8] = cmul(v[8], w8);
+  v[9] = cmul(v[9], cmul(w8, w1));
+  v[10] = cmul(v[10], cmul(w8, w2));
+  v[11] = cmul(v[11], cmul(w8, w3));
+  v[12] = cmul(v[12], cmul(w8, w4));
+  v[13] = cmul(v[13], cmul(w8, w5));
+  v[14] = cmul(v[14], cmul(w8, w6));
+  v[15] = cmul(v[15], cmul(w8, w7));
+}
+
+template <int R, int DIR>
+__device__ __forceinline__ void apply_tw_small(float2* v, const float2* b) {
+  if constexpr (R == 2) {
+    v[1] = cmul(v[1], twd<DIR>(b[0]));
+  } else if constexpr (R == 4) {
+    const float2 w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
+    v[1] = cmul(v[1], w1);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], cmul(w1, w2));
+  } else {
+    const float2 w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
+    const float2 w4 = twd<DIR>(opaque(b[2]));
+    const float2 w3 = cmul(w1, w2);
+    v[1] = cmul(v[1], w1);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], w3);
+    v[4] = cmul(v[4], w4);
+    v[5] = cmul(v[5], cmul(w4, w1));
+    v[6] = cmul(v[6], cmul(w4, w2));
+    v[7] = cmul(v[7], cmul(w4, w3));
+  }
+}
+
+// In-place FFT of one row.  v[m] holds position t + m*NT on entry and exit.
+// lds: this row's region of buffer 0; bufstride: offset (in float2) of buffer 1
+// when NBUF == 2.  par: running buffer parity (NBUF == 2), shared by all calls of
+// the workgroup in the same order.  Every thread of the workgroup must call this
+// the same number of times (it contains __syncthreads()).
+template <int LOGN, int DIR, int NBUF>
+__device__ __forceinline__ void fft_row(float2 (&v)[16], float2* __restrict__ lds, int bufstride,
+                                        const float2* tw, int t, int& par) {
+  using P = FftPlan<LOGN>;
+  constexpr bool kAligned = (P::NT % 16) == 0;  // strides are multiples of 16 -> pad is additive
+  dft16<DIR>(v);
+  if constexpr (P::NPASS == 1) return;
+  {
+    float2* buf = lds + (NBUF == 2 ? par * bufstride : 0);
+    if constexpr (NBUF == 1) __syncthreads();
+    float2* w = buf + 17 * t;  // lpad(16 t + r) = 17 t + r
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w[r] = v[r];
+    __syncthreads();
+  }
+  const int pt = lpad(t);
+  int ns = 16;
+#pragma unroll
+  for (int p = 1; p < P::NPASS; ++p) {
+    const bool last = (p == P::NPASS - 1);
+    const float2* rbuf = lds + (NBUF == 2 ? par * bufstride : 0);
+    if (p < P::P16) {
+      if constexpr (kAligned) {
+        const float2* rb = rbuf + pt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = rb[r * (P::NT + P::NT / 16)];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = rbuf[lpad(t + r * P::NT)];
+      }
+      if constexpr (NBUF == 2) par ^= 1;
+      apply_tw16<DIR>(v, tw + 4 * (p - 1));
+      dft16<DIR>(v);
+      if (!last) {
+        float2* wbuf = lds + (NBUF == 2 ? par * bufstride : 0);
+        const int idxD = (t / ns) * ns * 16 + (t & (ns - 1));
+        if constexpr (NBUF == 1) __syncthreads();
+        float2* wb = wbuf + lpad(idxD);  // ns >= 16 -> r*ns keeps the pad additive
+#pragma unroll
+        for (int r = 0; r < 16; ++r) wb[r * (ns + ns / 16)] = v[r];
+        __syncthreads();
+        ns *= 16;
+      }
+    } else {
+      constexpr int R = P::REM > 1 ? P::REM : 16;
+      constexpr int Q = 16 / R;
+      constexpr int tb = 4 * (P::P16 - 1);
+      constexpr int tstep = R == 2 ? 1 : (R == 4 ? 2 : 3);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if constexpr (kAligned) {
+            const int off = q * P::NT + r * (P::N / R);
+            v[q * R + r] = rbuf[pt + off + (off >> 4)];
+          } else {
+            v[q * R + r] = rbuf[lpad(t + q * P::NT + r * (P::N / R))];
+          }
+        }
+      if constexpr (NBUF == 2) par ^= 1;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        apply_tw_small<R, DIR>(v + q * R, tw + tb + tstep * q);
+        dft_small<R, DIR>(v + q * R);
+      }
+      // register q*R + r holds position t + (q + r*Q)*NT
+      float2 o[16];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[q + r * Q] = v[q * R + r];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = o[m];
+    }
+  }
+}
+
+}  // namespace wtmi

@@ -1,0 +1,325 @@
+// Wavelet coherence (K7 + K8 of DESIGN.md).
+//
+// Replaces the numerics of pycwt.wct(..., sig=False) as called from src/wct.py:106-118
+// (SURVEY Appendix A.4):
+//   W1, W2 = cwt(normalised y1, y2);  S1 = smooth(|W1|^2/s), S2 = smooth(|W2|^2/s),
+//   S12 = smooth(W12/s) with W12 = W1 conj(W2);  WCT = |S12|^2 / (S1 S2);
+//   aWCT = angle(W12)  -> arrows u = sin(aWCT), v = cos(aWCT)  (src/wct.py:143-158)
+// where Morlet.smooth = time Gaussian F = exp(-(s/dt)^2 k^2 / 2) applied by FFT on the
+// row zero-padded to N, then a [0.5, 1, .., 1, 0.5]/(K-1) boxcar over K scale rows
+// (scipy convolve2d 'same': rows i - K/2 .. i + (K-1)/2, zero outside).
+//
+// Phase A (one workgroup = one pair x a chunk of scales): per scale row two inverse
+// FFTs give W1, W2; |W1|^2 + i|W2|^2 and W12 are forward-transformed, multiplied by
+// F/(N s) (F is real and even, so the two real fields share one complex FFT) and
+// inverse-transformed: 6 in-LDS FFTs per row, the time-smoothed row
+// T = (T1, T2, Re T12, Im T12) goes to a float4 workspace.
+// Phase B (one thread = one time column of one pair): streams the S rows of T once,
+// keeps the last K rows in registers and writes WCT.
+#include "cwt_common.hpp"
+
+namespace wtmi {
+
+template <int LOGN>
+struct WctGeom {
+  using P = FftPlan<LOGN>;
+  static constexpr int ROWS = P::NT >= 256 ? 1 : 256 / P::NT;
+  static constexpr int BLOCK = P::NT * ROWS;
+  static constexpr int MINW = BLOCK >= 1024 ? 4 : (BLOCK >= 512 ? 2 : 2);
+};
+
+constexpr int kWctMaxChunk = 512;
+
+// bins this thread owns: kk = t + (m < 8 ? m : m - 16) * NT
+template <int LOGN>
+__device__ __forceinline__ void smooth_filter(float2 (&v)[16], float beta, float scale, int t) {
+  using P = FftPlan<LOGN>;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const float kk = static_cast<float>(t + (m < 8 ? m : m - 16) * P::NT);
+    const float f = scale * __builtin_amdgcn_exp2f(beta * kk * kk);
+    v[m] = cscale(v[m], f);
+  }
+}
+
+// Forward spectra of both series of every pair: spec[b][which][k], natural order.
+template <int LOGN>
+__global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, float2* __restrict__ spec) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  __shared__ float2 lds[G::ROWS * P::PADN];
+  const int tid = threadIdx.x;
+  const int g = tid / P::NT;
+  const int t = tid - g * P::NT;
+  // row group g handles series (pair, which) = blockIdx.x * ROWS + g
+  const long long item = static_cast<long long>(blockIdx.x) * G::ROWS + g;
+  const bool valid = item < 2 * a.batch;
+  const long long b = valid ? item >> 1 : 0;
+  const int which = static_cast<int>(item & 1);
+  float2 tw[P::NTW_ALLOC];
+  fft_twiddles<LOGN>(tw, t);
+  int par = 0;
+  float2 X[16];
+  if (which == 0)
+    load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
+  else
+    load_series<LOGN>(X, a.x2, a.affine2, b, a.ld, a.n0, t);
+  fft_row<LOGN, -1, 1>(X, lds + g * P::PADN, 0, tw, t, par);
+  if (!valid) return;
+  float2* o = spec + (2 * b + which) * static_cast<long long>(P::N);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) o[t + m * P::NT] = X[m];
+}
+
+// The spectra are loop-invariant: an opaque pointer stops the compiler from hoisting
+// the 2 x 16 loads out of the scale loop (which costs 64 VGPRs and spills).
+template <int LOGN>
+__device__ __forceinline__ void load_spec(float2 (&X)[16], const float2* row, int t) {
+  using P = FftPlan<LOGN>;
+  asm volatile("" : "+s"(row));
+#pragma unroll
+  for (int m = 0; m < 16; ++m) X[m] = row[t + m * P::NT];
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
+    wct_phase_a(CwtArgs a, const float2* __restrict__ spec, float4* __restrict__ T) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  __shared__ float2 lds[G::ROWS * P::PADN + 2 * kWctMaxChunk];
+  float2* prm_tab = lds + G::ROWS * P::PADN;      // (alpha, log2 c) of the Morlet filter
+  float2* smt_tab = prm_tab + kWctMaxChunk;       // (beta, 1/(N s)) of the time smoother
+  const int tid = threadIdx.x;
+  const int g = tid / P::NT;
+  const int t = tid - g * P::NT;
+  const long long blk = blockIdx.x;
+  const long long b = blk / a.nchunks;
+  const int ch = static_cast<int>(blk - b * a.nchunks);
+  const int j0 = ch * a.chunk;
+  const int j1 = min(a.S, j0 + a.chunk);
+  float2* my = lds + g * P::PADN;
+  constexpr int bufstride = 0;
+  const float2* spec1 = spec + 2 * b * static_cast<long long>(P::N);
+  const float2* spec2 = spec1 + P::N;
+
+  for (int i = tid; i < j1 - j0; i += G::BLOCK) {
+    const double s = a.scales[j0 + i];
+    prm_tab[i] = morlet_params(s, a.dt, P::N);
+    const double sn = s / a.dt * 2.0 * kPi / P::N;  // (s/dt) * (2 pi / N)
+    smt_tab[i] = make_float2(static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn),
+                             static_cast<float>(1.0 / (static_cast<double>(P::N) * s)));
+  }
+  float2 tw[P::NTW_ALLOC];
+  fft_twiddles<LOGN>(tw, t);
+  int par = 0;
+  __syncthreads();
+
+  const float f0 = static_cast<float>(a.f0);
+  const int iters = (j1 - j0 + G::ROWS - 1) / G::ROWS;
+  for (int it = 0; it < iters; ++it) {
+    const int jl = it * G::ROWS + g;
+    const bool valid = jl < j1 - j0;
+    const float2 prm = prm_tab[valid ? jl : 0];
+    const float2 smt = smt_tab[valid ? jl : 0];
+    float2 w1[16], v[16];
+    load_spec<LOGN>(w1, spec1, t);
+    morlet_filter<LOGN>(v, w1, prm, f0, t);
+    fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) w1[m] = v[m];
+    load_spec<LOGN>(v, spec2, t);
+    morlet_filter<LOGN>(v, v, prm, f0, t);
+    fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
+    const int j = j0 + jl;
+    const long long rowbase = (b * a.S + (valid ? j : j0)) * static_cast<long long>(a.n0);
+    float* urow = a.out_u ? a.out_u + rowbase : nullptr;
+    float* vrow = a.out_v ? a.out_v + rowbase : nullptr;
+    const bool arrows = valid && urow != nullptr;
+    // W12 -> arrows; build z1 = |W1|^2 + i |W2|^2 and z2 = W12 (zero past n0: the
+    // reference smooths the row zero-padded to N)
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int pos = t + m * P::NT;
+      const float2 w12 = cmul(w1[m], cconj(v[m]));
+      const bool in = pos < a.n0;
+      if (arrows && in) {
+        const float r = sqrtf(cabs2(w12));
+        urow[pos] = r > 0.f ? w12.y / r : 0.f;
+        vrow[pos] = r > 0.f ? w12.x / r : 1.f;
+      }
+      const float2 z1 = make_float2(cabs2(w1[m]), cabs2(v[m]));
+      w1[m] = in ? w12 : make_float2(0.f, 0.f);
+      v[m] = in ? z1 : make_float2(0.f, 0.f);
+    }
+    fft_row<LOGN, -1, 1>(v, my, bufstride, tw, t, par);
+    smooth_filter<LOGN>(v, smt.x, smt.y, t);
+    fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
+    fft_row<LOGN, -1, 1>(w1, my, bufstride, tw, t, par);
+    smooth_filter<LOGN>(w1, smt.x, smt.y, t);
+    fft_row<LOGN, 1, 1>(w1, my, bufstride, tw, t, par);
+    if (!valid) continue;
+    float4* trow = T + rowbase;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int pos = t + m * P::NT;
+      if (pos < a.n0) trow[pos] = make_float4(v[m].x, v[m].y, w1[m].x, w1[m].y);
+    }
+  }
+}
+
+// Scale boxcar + coherence.  Row i uses rows i - K/2 .. i + (K-1)/2 (zero outside),
+// end weights 0.5; the normalisation 1/(K-1) cancels in |S12|^2 / (S1 S2) but is kept
+// so the smoothed fields match the reference.
+template <int K>
+__global__ void __launch_bounds__(256) wct_phase_b(const float4* __restrict__ T, long long batch, int n0,
+                                                   int S, float* __restrict__ coh) {
+  const long long tiles = (n0 + 255) / 256;
+  const long long b = blockIdx.x / tiles;
+  const int tcol = static_cast<int>((blockIdx.x - b * tiles) * 256 + threadIdx.x);
+  if (tcol >= n0) return;
+  constexpr int LO = K / 2;        // rows before i
+  constexpr int HI = (K - 1) / 2;  // rows after i
+  const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
+  const float4* col = T + b * static_cast<long long>(S) * n0 + tcol;
+  float* out = coh + b * static_cast<long long>(S) * n0 + tcol;
+  float4 ring[K];
+#pragma unroll
+  for (int r = 0; r < K; ++r) ring[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // row j enters the ring at slot j % K; output row i = j - HI is complete then.
+  for (int jb = 0; jb < S + HI; jb += K) {
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int j = jb + r;
+      ring[r] = j < S ? col[static_cast<long long>(j) * n0] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int i = j - HI;
+      if (i >= 0 && i < S) {
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          // slot of row i - LO + q  (rows i-LO .. i+HI = j-K+1 .. j)
+          const int slot = (r + 1 + q) % K;
+          const float wq = (K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn;
+          const int row = i - LO + q;
+          if (row >= 0) {
+            acc.x = fmaf(wq, ring[slot].x, acc.x);
+            acc.y = fmaf(wq, ring[slot].y, acc.y);
+            acc.z = fmaf(wq, ring[slot].z, acc.z);
+            acc.w = fmaf(wq, ring[slot].w, acc.w);
+          }
+        }
+        out[static_cast<long long>(i) * n0] = (acc.z * acc.z + acc.w * acc.w) / (acc.x * acc.y);
+      }
+    }
+  }
+}
+
+template <int LOGN>
+static int launch_phase_a(CwtArgs& a, float2* spec, float4* T, hipStream_t st) {
+  using G = WctGeom<LOGN>;
+  {
+    const long long items = 2 * a.batch;
+    const long long sgrid = (items + G::ROWS - 1) / G::ROWS;
+    if (sgrid > 0x7fffffffll) return kErrUnsupported;
+    hipLaunchKernelGGL(wct_spectra<LOGN>, dim3(static_cast<unsigned>(sgrid)), dim3(G::BLOCK), 0, st, a,
+                       spec);
+    const int rc = launch_status();
+    if (rc != kOk) return rc;
+  }
+  const int rows = G::ROWS;
+  long long want = (4096 + a.batch - 1) / a.batch;
+  const int max_chunks = (a.S + 4 * rows - 1) / (4 * rows);
+  int nch = static_cast<int>(want < 1 ? 1 : want);
+  if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
+  int chunk = (a.S + nch - 1) / nch;
+  chunk = ((chunk + rows - 1) / rows) * rows;
+  if (chunk > kWctMaxChunk) chunk = kWctMaxChunk;
+  nch = (a.S + chunk - 1) / chunk;
+  a.nchunks = nch;
+  a.chunk = chunk;
+  const long long grid = a.batch * nch;
+  if (grid > 0x7fffffffll) return kErrUnsupported;
+  hipLaunchKernelGGL(wct_phase_a<LOGN>, dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, T);
+  return launch_status();
+}
+
+template <int K>
+static int launch_phase_b(const float4* T, long long batch, int n0, int S, float* coh, hipStream_t st) {
+  const long long tiles = (n0 + 255) / 256;
+  const long long grid = batch * tiles;
+  if (grid > 0x7fffffffll) return kErrUnsupported;
+  hipLaunchKernelGGL(wct_phase_b<K>, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, T, batch, n0,
+                     S, coh);
+  return launch_status();
+}
+
+static int log2_ceil_w(long long n) {
+  int l = 0;
+  while ((1ll << l) < n) ++l;
+  return l;
+}
+
+}  // namespace wtmi
+
+using namespace wtmi;
+
+// workspace = [T: batch x S x n0 float4][spectra: batch x 2 x N float2]
+static long long wct_t_bytes(long long batch, long long n0, int n_scales) {
+  const long long b = batch * n0 * static_cast<long long>(n_scales) * static_cast<long long>(sizeof(float4));
+  return (b + 255) & ~255ll;
+}
+
+extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales) {
+  if (batch < 0 || n0 < 0 || n_scales < 0) return -1;
+  const long long N = 1ll << log2_ceil_w(n0 < 1 ? 1 : n0);
+  return wct_t_bytes(batch, n0, n_scales) + batch * 2 * N * static_cast<long long>(sizeof(float2));
+}
+
+extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
+                               long long n0, const double* affine1, const double* affine2,
+                               const double* scales, int n_scales, double dt, double f0, int boxcar,
+                               void* workspace, float* out_coh, float* out_u, float* out_v,
+                               void* stream) {
+  if (!x1 || !x2 || !scales || !workspace || !out_coh || n0 < 0 || batch < 0 || n_scales < 0 ||
+      ld < n0 || boxcar < 1)
+    return kErrArg;
+  if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
+  if (n0 > (1 << 14) || boxcar > 24) return kErrUnsupported;
+  if (batch == 0 || n0 == 0 || n_scales == 0) return kOk;
+  const int logn = log2_ceil_w(n0);
+  if (logn < 4) return kErrUnsupported;  // n0 <= 8: below the FFT engine's minimum row
+  CwtArgs a{};
+  a.x = x1;
+  a.x2 = x2;
+  a.ld = ld;
+  a.batch = batch;
+  a.n0 = static_cast<int>(n0);
+  a.S = n_scales;
+  a.affine = affine1;
+  a.affine2 = affine2;
+  a.scales = scales;
+  a.dt = dt;
+  a.f0 = f0;
+  a.out_u = out_u;
+  a.out_v = out_v;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float4* T = static_cast<float4*>(workspace);
+  float2* spec = reinterpret_cast<float2*>(static_cast<char*>(workspace) + wct_t_bytes(batch, n0, n_scales));
+  int rc;
+  switch (logn) {
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, T, st); break;
+    WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
+    WTMI_A(12) WTMI_A(13) WTMI_A(14)
+#undef WTMI_A
+    default: return kErrUnsupported;
+  }
+  if (rc != kOk) return rc;
+  const int n0i = static_cast<int>(n0);
+  switch (boxcar) {
+#define WTMI_B(K) case K: return launch_phase_b<K>(T, batch, n0i, n_scales, out_coh, st);
+    WTMI_B(1) WTMI_B(2) WTMI_B(3) WTMI_B(4) WTMI_B(5) WTMI_B(6) WTMI_B(7) WTMI_B(8)
+    WTMI_B(9) WTMI_B(10) WTMI_B(11) WTMI_B(12) WTMI_B(13) WTMI_B(14) WTMI_B(15) WTMI_B(16)
+    WTMI_B(17) WTMI_B(18) WTMI_B(19) WTMI_B(20) WTMI_B(21) WTMI_B(22) WTMI_B(23) WTMI_B(24)
+#undef WTMI_B
+    default: return kErrUnsupported;
+  }
+}

@@ -1,0 +1,101 @@
+"""Continuous wavelet transform of one series (reference: src/cwt.py).
+
+Same constants, dataclasses and ``run_cwt`` signature as the reference
+(src/cwt.py:37-135); the transform, |W|^2 and the significance ratio are produced
+by one fused HIP kernel (``wtmi_cwt_morlet``), standardisation and the AR(1)
+covariances by the moments/affine kernels.  Reference quirks kept:
+``normalize`` is a no-op (B.1), AR(1) uses ``y_values`` not the standardised series
+(B.2), significance uses variance 1.0 and the module constants DT/DJ/S0/J (B.3).
+"""
+
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import List, Type
+
+import numpy as np
+import numpy.typing as npt
+import torch
+
+from wtmi import ops, transforms
+from wtmi.wavelets import Morlet, as_morlet
+
+logger = logging.getLogger(__name__)
+
+UNITS = "%"
+NORMALIZE = True
+DT = 1 / 12  # In years
+S0 = 2 * DT  # Starting scale
+DJ = 1 / 12  # Twelve sub-octaves per octaves
+J = 7 / DJ  # Seven powers of two with DJ sub-octaves
+MOTHER = Morlet(f0=6)
+LEVELS = [0.0625, 0.125, 0.25, 0.5, 1, 2, 4, 8, 16]
+
+
+@dataclass
+class DataForCWT:
+    """Holds data for continuous wavelet transform"""
+
+    t_values: npt.NDArray
+    y_values: npt.NDArray
+    mother_wavelet: Type
+    delta_t: float
+    delta_j: float
+    initial_scale: float
+    levels: List[float]
+    time_range: npt.NDArray = field(init=False)
+
+    def __post_init__(self):
+        # reference quirk B.4: the method is shadowed by its own result
+        self.time_range = self.time_range(self)
+
+    def time_range(self) -> npt.NDArray:
+        t0 = min(self.t_values)
+        t0 = t0.astype("datetime64[Y]").astype(int) + 1970
+        num_observations = self.t_values.size
+        self.time_range = np.arange(1, num_observations + 1) * self.delta_t + t0
+        return np.arange(1, num_observations + 1) * self.delta_t + t0
+
+
+@dataclass
+class ResultsFromCWT:
+    """Holds results from continuous wavelet transform"""
+
+    power: npt.NDArray
+    period: npt.NDArray
+    significance_levels: npt.NDArray
+    coi: npt.NDArray
+
+
+def run_cwt(cwt_data: Type[DataForCWT], normalize: bool = True, standardize: bool = False,
+            calculate_significance: bool = True, significance_level: float = 0.95,
+            **kwargs) -> Type[ResultsFromCWT]:
+    """Conducts Continuous Wavelet Transform.
+    Returns power spectrum, period, cone of influence, and significance levels."""
+    mother = as_morlet(cwt_data.mother_wavelet)
+    y = transforms._to_dev(np.asarray(cwt_data.y_values)).reshape(1, -1)
+    mom_y = ops.series_moments(y)
+    if standardize:
+        kw = {k: kwargs[k] for k in ("detrend", "standardize", "remove_mean") if k in kwargs}
+        coef = transforms.standardize_coefs(mom_y, **kw)
+        x32 = ops.affine(y, coef, torch.float32)
+    else:  # quirk B.1: `normalize` has no effect
+        x32 = ops.affine(y, torch.tensor([[0.0, 0.0, 1.0]], dtype=torch.float64, device=y.device),
+                         torch.float32)
+    m = transforms._np(mom_y)[0]
+    alpha, _, _ = transforms._ar1_from_moments(m[4], m[5], int(m[6]))  # quirk B.2
+
+    n0 = y.shape[1]
+    sj, freqs = transforms.scales_for(n0, DT, DJ, S0, J, mother)
+    sig_scale = None
+    if calculate_significance:
+        signif, _ = transforms.significance(1.0, DT, sj, 0, alpha,
+                                            significance_level=significance_level, wavelet=mother)
+        sig_scale = 1.0 / signif
+    res = ops.cwt_morlet(x32, sj, DT, mother.f0, sig_scale=sig_scale, want_w=False,
+                         want_power=True, want_sig=calculate_significance)
+    power = transforms._np(res["power"][0], np.float64)
+    sig = transforms._np(res["sig"][0], np.float64) if calculate_significance else None
+    coi = transforms.cone_of_influence(n0, DT, mother)
+    return ResultsFromCWT(power, 1 / freqs, sig, coi)

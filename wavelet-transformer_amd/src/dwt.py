@@ -1,0 +1,91 @@
+"""Smoothing of signals via wavelet reconstruction (reference: src/dwt.py).
+
+Pyramid DWT / inverse DWT (mode 'symmetric') run on the GPU (``wtmi_wavedec`` /
+``wtmi_waverec``).  ``ResultsFromDWT.smooth_signal`` reconstructs all ``levels``
+smoothed signals in ONE batched launch (one variant per level) instead of the
+reference's loop of ``pywt.waverec`` calls (src/dwt.py:53-73).  Coefficient lists
+keep pywt order ``[cA_J, cD_J, ..., cD_1]`` (quirk B.10).
+"""
+
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import Dict, Type
+
+import numpy as np
+import numpy.typing as npt
+
+from wtmi import transforms
+from wtmi.wavelets import Wavelet, as_filter_bank
+
+logger = logging.getLogger(__name__)
+
+MOTHER = Wavelet("db4")
+
+
+@dataclass
+class DataForDWT:
+    """Holds data for discrete wavelet transform"""
+
+    y_values: npt.NDArray
+    mother_wavelet: Type
+    levels: int = None
+
+
+@dataclass
+class ResultsFromDWT:
+    """`coeffs`: transform coefficients; `levels`: levels applied;
+    `smoothed_signal_dict`: smoothed signal for each level"""
+
+    coeffs: npt.NDArray
+    levels: int
+    smoothed_signal_dict: Dict[int, Dict[str, npt.NDArray]] = field(default_factory=dict)
+
+    def smooth_signal(self, y_values: npt.NDArray, mother_wavelet: Type
+                      ) -> Dict[int, Dict[str, npt.NDArray]]:
+        """signal_dict[l]: reconstruction with the last l detail arrays zeroed."""
+        nlist = len(self.coeffs)
+        full = (1 << nlist) - 1
+        lv = list(range(self.levels, 0, -1))
+        masks = []
+        for lvl in lv:
+            m = full
+            for k in range(1, lvl + 1):
+                m &= ~(1 << (nlist - k))
+            masks.append(m)
+        recs = transforms.waverec_variants(self.coeffs, mother_wavelet, masks)
+        signals_dict = {}
+        for i, lvl in enumerate(lv):
+            print(f"s_{lvl} stored with key {lvl}")  # reference prints too (quirk B.12)
+            smooth_coeffs = [np.array(c, copy=True) for c in self.coeffs]
+            for k in range(1, lvl + 1):
+                smooth_coeffs[-k] = np.zeros_like(smooth_coeffs[-k])
+            signals_dict[lvl] = {"coeffs": smooth_coeffs, "signal": trim_signal(y_values, recs[i])}
+        self.smoothed_signal_dict = signals_dict
+
+
+def trim_signal(original_signal: npt.NDArray, reconstructed: npt.NDArray) -> npt.NDArray:
+    """Drop the FIRST reconstructed sample for odd-length inputs (quirk B.12)."""
+    if len(original_signal) % 2 != 0:
+        logger.warning("Trimming signal at beginning")
+        return reconstructed[1:]
+    return reconstructed
+
+
+def run_dwt(dwt_data: Type[DataForDWT]) -> Type[ResultsFromDWT]:
+    """Coefficients from a pyramid DWT; ``levels=None`` means pywt's maximum level."""
+    w = as_filter_bank(dwt_data.mother_wavelet)
+    if dwt_data.levels is None:
+        dwt_levels = transforms.dwt_max_level(len(dwt_data.y_values), w.dec_len)
+        print(f"""Max decomposition level of {dwt_levels} for time series length
+            of {len(dwt_data.y_values)}""")
+    else:
+        dwt_levels = dwt_data.levels
+    coeffs = transforms.wavedec(dwt_data.y_values, w, level=dwt_data.levels)
+    return ResultsFromDWT(coeffs, dwt_levels)
+
+
+def reconstruct_signal_component(signal_coeffs: list, wavelet: str, level: int):
+    """Inverse DWT keeping only list entry ``level`` (src/dwt.py:110-120)."""
+    return transforms.waverec_variants(signal_coeffs, wavelet, [1 << level])[0]

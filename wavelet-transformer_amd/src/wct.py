@@ -1,0 +1,107 @@
+"""Wavelet coherence of two series (reference: src/wct.py).
+
+``run_wct`` keeps the reference signature, including the misspelled keyword
+``calculate_signficance`` (src/wct.py:96-140).  Coherence and phase arrows come from
+the fused coherence kernels (``wtmi_wct_morlet``).  With significance off the
+reference divides by ``signif = [0]`` and returns an all-inf ratio (quirk B.8);
+that is reproduced.  Significance ON needs pycwt's Monte-Carlo
+``wct_significance`` -- SURVEY 8(f) row 1, not built yet: it raises
+NotImplementedError.
+"""
+
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import List, Tuple, Type
+
+import numpy as np
+import numpy.typing as npt
+import torch
+
+from wtmi import ops, transforms
+from wtmi.wavelets import Morlet, as_morlet
+
+logger = logging.getLogger(__name__)
+
+DT = 1 / 12
+DJ = 1 / 8
+S0 = 2 * DT
+MOTHER = "morlet"
+MOTHER_DICT = {"morlet": Morlet(6)}
+LEVELS = [0.0625, 0.125, 0.25, 0.5, 1, 2, 4, 8, 16]
+WCT_LEVELS = [0.0, 0.125, 0.25, 0.375, 0.5, 0.625, 0.75, 0.875, 1.0]
+
+WCT_PLOT_PROPS = {
+    "cmap": "jet", "sig_colors": "k", "sig_linewidths": 2, "coi_color": "k", "coi_alpha": 0.3,
+    "coi_hatch": "--", "phase_diff_units": "width", "phase_diff_angles": "uv",
+    "phase_diff_pivot": "mid", "phase_diff_linewidth": 0.5, "phase_diff_edgecolor": "k",
+    "phase_diff_alpha": 0.7,
+}
+
+
+@dataclass
+class DataForWCT:
+    """Holds data for WCT"""
+
+    t_values: npt.NDArray = field(init=False)
+    y1_values: npt.NDArray
+    y2_values: npt.NDArray
+    mother_wavelet: Type
+    delta_t: float
+    delta_j: float
+    initial_scale: float
+    levels: List[float]
+    actual_times: npt.NDArray = None
+
+    def __post_init__(self):
+        if self.actual_times is not None:
+            self.t_values = self.actual_times
+        else:
+            self.t_values = np.linspace(1, self.y1_values.size + 1, self.y1_values.size)
+
+
+@dataclass
+class ResultsFromWCT:
+    """Holds results from Wavelet Coherence Transform"""
+
+    coherence: npt.NDArray
+    period: npt.NDArray
+    significance_levels: npt.NDArray
+    coi: npt.NDArray
+    phase_diff_u: npt.NDArray
+    phase_diff_v: npt.NDArray
+
+
+def run_wct(wavelet_coherence_transform: Type[DataForWCT], calculate_signficance: bool = True,
+            significance_level: float = 0.95) -> Type[ResultsFromWCT]:
+    """Coherence magnitude, period, significance ratio, cone of influence and phase."""
+    d = wavelet_coherence_transform
+    mother = as_morlet(d.mother_wavelet)
+    y1, y2 = np.asarray(d.y1_values), np.asarray(d.y2_values)
+    if y1.size != y2.size:
+        raise AssertionError("Input signals must have the same size")
+    if calculate_signficance:
+        raise NotImplementedError(
+            "run_wct(calculate_signficance=True) needs the Monte-Carlo wct_significance "
+            "(SURVEY 8(f) row 1), not implemented yet")
+    d1 = transforms._to_dev(y1).reshape(1, -1)
+    d2 = transforms._to_dev(y2).reshape(1, -1)
+    x1 = ops.affine(d1, transforms.normalize_coefs(ops.series_moments(d1)), torch.float32)
+    x2 = ops.affine(d2, transforms.normalize_coefs(ops.series_moments(d2)), torch.float32)
+    res, sj, freqs = transforms.wct_batch(x1, x2, d.delta_t, d.delta_j, d.initial_scale, -1, mother,
+                                          normalize=False, want_uv=True)
+    n0 = y1.size
+    coherence = transforms._np(res["coh"][0], np.float64)
+    signif = np.asarray([0])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sig95 = np.abs(coherence) / (np.ones([1, n0]) * signif[:, None])
+    coi = transforms.cone_of_influence(n0, d.delta_t, mother)
+    u = transforms._np(res["u"][0], np.float64)
+    v = transforms._np(res["v"][0], np.float64)
+    return ResultsFromWCT(coherence, 1 / freqs, sig95, coi, u, v)
+
+
+def calculate_phase_difference(wct_phase: npt.NDArray) -> Tuple[npt.NDArray, npt.NDArray]:
+    angle = 0.5 * np.pi - wct_phase
+    return np.cos(angle), np.sin(angle)

@@ -1,0 +1,121 @@
+"""Cross-wavelet transform of two series (reference: src/xwt.py).
+
+``run_xwt`` keeps the reference signature (src/xwt.py:83-139).  Power |W1 W2*|^2 and
+the significance ratio come from one pair-mode HIP kernel launch; the phase arrows
+from a second launch at the scales pycwt.wct would use -- the reference passes
+``delta_j=`` to ``wct`` which swallows it, so the phase runs at dj = 1/12
+(quirk B.5).  ``normalize=False`` raises NameError in the reference (B.7); here it
+returns the raw complex cross spectrum (documented deviation).
+"""
+
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import List, Tuple, Type
+
+import numpy as np
+import numpy.typing as npt
+import torch
+
+from wtmi import ops, transforms
+from wtmi.wavelets import Morlet, as_morlet
+from src.utils.wavelet_helpers import coi_polygon
+
+logger = logging.getLogger(__name__)
+
+DT = 1 / 12
+DJ = 1 / 8
+S0 = 2 * DT
+MOTHER = "morlet"
+MOTHER_DICT = {"morlet": Morlet(6)}
+LEVELS = [0.0625, 0.125, 0.25, 0.5, 1, 2, 4, 8, 16]
+
+XWT_PLOT_PROPS = {
+    "cmap": "jet", "sig_colors": "k", "sig_linewidths": 2, "coi_color": "k", "coi_alpha": 0.3,
+    "coi_hatch": "--", "phase_diff_units": "width", "phase_diff_angles": "uv",
+    "phase_diff_pivot": "mid", "phase_diff_linewidth": 0.5, "phase_diff_edgecolor": "k",
+    "phase_diff_alpha": 0.7,
+}
+
+
+@dataclass
+class DataForXWT:
+    """Holds data for XWT"""
+
+    t_values: npt.NDArray = field(init=False)
+    y1_values: npt.NDArray
+    y2_values: npt.NDArray
+    mother_wavelet: Type
+    delta_t: float
+    delta_j: float
+    initial_scale: float
+    levels: List[float]
+
+    def __post_init__(self):
+        self.t_values = np.linspace(1, self.y1_values.size + 1, self.y1_values.size)
+
+
+@dataclass
+class ResultsFromXWT:
+    """Holds results from Cross-Wavelet Transform"""
+
+    power: npt.NDArray
+    period: npt.NDArray
+    significance_levels: npt.NDArray
+    coi: npt.NDArray
+    phase_diff_u: npt.NDArray
+    phase_diff_v: npt.NDArray
+
+
+def _pair(y1, y2):
+    d1 = transforms._to_dev(np.asarray(y1)).reshape(1, -1)
+    d2 = transforms._to_dev(np.asarray(y2)).reshape(1, -1)
+    m1, m2 = ops.series_moments(d1), ops.series_moments(d2)
+    return d1, d2, m1, m2
+
+
+def run_xwt(cross_wavelet_transform: Type[DataForXWT], normalize: bool = True
+            ) -> Type[ResultsFromXWT]:
+    """Cross-wavelet power, period, significance ratio, COI polygon and phase arrows."""
+    d = cross_wavelet_transform
+    mother = as_morlet(d.mother_wavelet)
+    y1, y2 = np.asarray(d.y1_values), np.asarray(d.y2_values)
+    d1, d2, m1, m2 = _pair(y1, y2)
+    n0 = d1.shape[1]
+    # pycwt.xwt(normalize=True): (y - mean) / std, in fp64 on the GPU
+    x1 = ops.affine(d1, transforms.normalize_coefs(m1), torch.float32)
+    x2 = ops.affine(d2, transforms.normalize_coefs(m2), torch.float32)
+    sj, freqs = transforms.scales_for(n0, d.delta_t, d.delta_j, d.initial_scale, -1, mother)
+    mh1, mh2 = transforms._np(m1)[0], transforms._np(m2)[0]
+    g1, _, _ = transforms._ar1_from_moments(mh1[4], mh1[5], int(mh1[6]))
+    g2, _, _ = transforms._ar1_from_moments(mh2[4], mh2[5], int(mh2[6]))
+    Pk1 = transforms.ar1_spectrum(freqs * d.delta_t, g1)
+    Pk2 = transforms.ar1_spectrum(freqs * d.delta_t, g2)
+    dof = mother.dofmin
+    signif = (Pk1 * Pk2) ** 0.5 * transforms._chi2_ppf(0.95, dof) / dof  # std1 = std2 = 1
+    period = 1 / freqs
+    coi = transforms.cone_of_influence(n0, d.delta_t, mother)
+    if normalize:
+        r = ops.xwt_morlet(x1, x2, sj, d.delta_t, mother.f0, sig_scale=1.0 / signif,
+                           want_power=True, want_sig=True)
+        power = transforms._np(r["power"][0], np.float64)
+        sig95 = transforms._np(r["sig"][0], np.float64)
+        coi_plot = coi_polygon(coi, period, np.log2(d.levels[2]))
+    else:
+        r = ops.xwt_morlet(x1, x2, sj, d.delta_t, mother.f0, want_w12=True)
+        power = transforms._np(r["w12"][0], np.complex128)
+        sig95 = power / (np.ones([1, n0]) * signif[:, None])
+        coi_plot = coi
+    # phase: pycwt.wct(..., delta_j=...) runs at its default dj = 1/12 (quirk B.5)
+    sj_p, _ = transforms.scales_for(n0, d.delta_t, 1 / 12, d.initial_scale, -1, mother)
+    rp = ops.xwt_morlet(x1, x2, sj_p, d.delta_t, mother.f0, want_uv=True)
+    u = transforms._np(rp["u"][0], np.float64)
+    v = transforms._np(rp["v"][0], np.float64)
+    return ResultsFromXWT(power, period, sig95, coi_plot, u, v)
+
+
+def calculate_phase_difference(xwt_phase: npt.NDArray) -> Tuple[npt.NDArray, npt.NDArray]:
+    """Arrow components (Torrence & Webster 1999): u = cos(pi/2 - phase), v = sin(...)."""
+    angle = 0.5 * np.pi - xwt_phase
+    return np.cos(angle), np.sin(angle)

@@ -1,0 +1,77 @@
+"""ctypes binding of libwtmi.so (the C ABI declared in include/wtmi.h).
+
+This is the reference-side binding a maintainer adds: the
+reference is pure Python, so the FFI is ctypes.  The library is loaded from the
+package directory (built in-tree by ``wtmi/build.py``); there is NO fallback --
+a missing or unloadable library raises immediately.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwtmi.so")
+
+_P = C.c_void_p
+_I64 = C.c_longlong
+_I32 = C.c_int
+_F64 = C.c_double
+_U64 = C.c_ulonglong
+
+# name -> (restype, argtypes); mirrors include/wtmi.h exactly
+PROTOTYPES = {
+    "wtmi_cwt_morlet": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _F64, _F64, _P, _P, _P, _P, _P]),
+    "wtmi_xwt_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _P,
+                               _P, _P, _P, _P, _P, _P]),
+    "wtmi_wct_workspace_bytes": (_I64, [_I64, _I64, _I32]),
+    "wtmi_wct_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _I32,
+                               _P, _P, _P, _P, _P]),
+    "wtmi_modwt": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _I32, _P, _P]),
+    "wtmi_imodwt": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _U64, _P, _I64, _P]),
+    "wtmi_dwt_lengths": (_I64, [_I64, _I32, _I32, _P]),
+    "wtmi_wavedec": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _I32, _P, _P]),
+    "wtmi_waverec": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _P]),
+    "wtmi_series_moments": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P]),
+    "wtmi_affine": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I64, _P]),
+}
+
+ERRORS = {-1: "invalid argument", -2: "unsupported size"}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class WtmiError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    """Load libwtmi.so once (thread-safe)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise WtmiError(
+                    f"{LIB_PATH} not found: build it with "
+                    "`python wavelet-transformer_amd/wtmi/build.py` (no CPU fallback exists)")
+            lib = C.CDLL(LIB_PATH, mode=C.RTLD_LOCAL)
+            for name, (res, args) in PROTOTYPES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def call(name: str, *args) -> int:
+    fn = getattr(load(), name)
+    rc = fn(*args)
+    if PROTOTYPES[name][0] is _I32 and rc != 0:
+        msg = ERRORS.get(rc, f"HIP error {rc}")
+        raise WtmiError(f"{name} failed: {msg}")
+    return rc

@@ -1,0 +1,279 @@
+"""Batched device-tensor API over libwtmi.so.
+
+Every function takes/returns torch tensors resident on an MI355X (``cuda`` device
+under ROCm), enqueues the HIP kernels on the current stream of that device and
+returns without synchronising.  There is no CPU implementation: a CPU tensor or a
+missing library raises.  The same functions are registered as torch custom ops
+(``torch.ops.wtmi.*``, see ``_register``) so they compose with torch code.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+
+VP = C.c_void_p
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return VP(t.data_ptr()) if t is not None else VP(None)
+
+
+def _stream(dev: torch.device):
+    return VP(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _check_dev(*ts):
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                f"wtmi kernels run on the GPU only; got a tensor on {t.device} "
+                "(no CPU fallback exists)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError("all wtmi operands must be on the same device")
+    return dev
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    """[n] or [B, n] -> [B, n] with unit stride along time."""
+    if x.dim() == 1:
+        x = x.unsqueeze(0)
+    if x.dim() != 2:
+        raise ValueError("expected a [batch, n] tensor")
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    return x
+
+
+def _f64_dev(a, dev) -> Optional[torch.Tensor]:
+    if a is None:
+        return None
+    if isinstance(a, torch.Tensor):
+        return a.to(device=dev, dtype=torch.float64).contiguous()
+    return torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)
+
+
+# ------------------------------------------------------------------------ moments
+def series_moments(x: torch.Tensor) -> torch.Tensor:
+    """[B, 8] float64: mean, std(ddof 0), slope, intercept, c0, c1, n, 0."""
+    x = _rows(x)
+    dev = _check_dev(x)
+    if x.dtype not in (torch.float32, torch.float64):
+        x = x.to(torch.float64)
+    out = torch.empty((x.shape[0], 8), dtype=torch.float64, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_series_moments", _ptr(x), int(x.dtype == torch.float64), x.stride(0),
+                  x.shape[0], x.shape[1], _ptr(out), _stream(dev))
+    return out
+
+
+def affine(x: torch.Tensor, coef: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    """y = (x - a0 - a1 t) * a2 per series (coef [B, 3] float64), computed in fp64."""
+    x = _rows(x)
+    dev = _check_dev(x, coef)
+    if x.dtype not in (torch.float32, torch.float64):
+        x = x.to(torch.float64)
+    coef = coef.to(torch.float64).contiguous()
+    y = torch.empty(x.shape, dtype=dtype, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_affine", _ptr(x), int(x.dtype == torch.float64), x.stride(0), x.shape[0],
+                  x.shape[1], _ptr(coef), _ptr(y), int(dtype == torch.float64), y.stride(0),
+                  _stream(dev))
+    return y
+
+
+# ---------------------------------------------------------------------------- CWT
+def cwt_morlet(x: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
+               affine: Optional[torch.Tensor] = None, sig_scale=None,
+               want_w: bool = True, want_power: bool = False, want_sig: bool = False,
+               out_w: Optional[torch.Tensor] = None):
+    """Morlet CWT of every row of x (float32 [B, n0]) at the given scales.
+
+    Returns a dict with any of ``w`` (complex64 [B, S, n0]), ``power`` and ``sig``
+    (float32 [B, S, n0], sig = power * sig_scale[j]).
+    """
+    x = _rows(x)
+    dev = _check_dev(x, affine)
+    if x.dtype != torch.float32:
+        x = x.to(torch.float32)
+    B, n0 = x.shape
+    sc = _f64_dev(scales, dev)
+    S = sc.numel()
+    ss = _f64_dev(sig_scale, dev) if want_sig else None
+    if want_sig and ss is None:
+        raise ValueError("want_sig needs sig_scale")
+    res = {}
+    if want_w:
+        if out_w is None:
+            out_w = torch.empty((B, S, n0), dtype=torch.complex64, device=dev)
+        res["w"] = out_w
+    if want_power:
+        res["power"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
+    if want_sig:
+        res["sig"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
+    aff = affine.to(torch.float64).contiguous() if affine is not None else None
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_cwt_morlet", _ptr(x), x.stride(0), B, n0, _ptr(aff), _ptr(sc), S,
+                  float(dt), float(f0), _ptr(ss), _ptr(res.get("w")), _ptr(res.get("power")),
+                  _ptr(res.get("sig")), _stream(dev))
+    return res
+
+
+def xwt_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
+               affine1=None, affine2=None, sig_scale=None, want_w12=False, want_power=False,
+               want_sig=False, want_uv=False):
+    """Cross-wavelet outputs of row pairs: any of w12 (complex64), power, sig, u, v."""
+    x1 = _rows(x1).to(torch.float32)
+    x2 = _rows(x2).to(torch.float32)
+    if x1.shape != x2.shape:
+        raise ValueError("x1 and x2 must have the same shape")
+    if x1.stride(0) != x2.stride(0):
+        x1, x2 = x1.contiguous(), x2.contiguous()
+    dev = _check_dev(x1, x2, affine1, affine2)
+    B, n0 = x1.shape
+    sc = _f64_dev(scales, dev)
+    S = sc.numel()
+    ss = _f64_dev(sig_scale, dev) if want_sig else None
+    shape = (B, S, n0)
+    res = {}
+    if want_w12:
+        res["w12"] = torch.empty(shape, dtype=torch.complex64, device=dev)
+    if want_power:
+        res["power"] = torch.empty(shape, dtype=torch.float32, device=dev)
+    if want_sig:
+        res["sig"] = torch.empty(shape, dtype=torch.float32, device=dev)
+    if want_uv:
+        res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
+        res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
+    a1 = affine1.to(torch.float64).contiguous() if affine1 is not None else None
+    a2 = affine2.to(torch.float64).contiguous() if affine2 is not None else None
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_xwt_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
+                  _ptr(sc), S, float(dt), float(f0), _ptr(ss), _ptr(res.get("w12")),
+                  _ptr(res.get("power")), _ptr(res.get("sig")), _ptr(res.get("u")),
+                  _ptr(res.get("v")), _stream(dev))
+    return res
+
+
+def wct_workspace_bytes(batch: int, n0: int, n_scales: int) -> int:
+    return int(_lib.call("wtmi_wct_workspace_bytes", batch, n0, n_scales))
+
+
+def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
+               boxcar: int, affine1=None, affine2=None, want_uv: bool = True,
+               workspace: Optional[torch.Tensor] = None):
+    """Wavelet coherence of row pairs; returns dict coh [B,S,n0] (+ u, v)."""
+    x1 = _rows(x1).to(torch.float32)
+    x2 = _rows(x2).to(torch.float32)
+    if x1.shape != x2.shape:
+        raise ValueError("x1 and x2 must have the same shape")
+    if x1.stride(0) != x2.stride(0):
+        x1, x2 = x1.contiguous(), x2.contiguous()
+    dev = _check_dev(x1, x2, affine1, affine2)
+    B, n0 = x1.shape
+    sc = _f64_dev(scales, dev)
+    S = sc.numel()
+    need = wct_workspace_bytes(B, n0, S)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    shape = (B, S, n0)
+    res = {"coh": torch.empty(shape, dtype=torch.float32, device=dev)}
+    if want_uv:
+        res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
+        res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
+    a1 = affine1.to(torch.float64).contiguous() if affine1 is not None else None
+    a2 = affine2.to(torch.float64).contiguous() if affine2 is not None else None
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_wct_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
+                  _ptr(sc), S, float(dt), float(f0), int(boxcar), _ptr(workspace),
+                  _ptr(res["coh"]), _ptr(res.get("u")), _ptr(res.get("v")), _stream(dev))
+    return res
+
+
+# -------------------------------------------------------------------------- MODWT
+def _taps(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def modwt(x: torch.Tensor, dec_lo, dec_hi, level: int) -> torch.Tensor:
+    """[B, n] float32 -> [B, level + 1, n] rows [W_1 .. W_J, V_J]."""
+    x = _rows(x).to(torch.float32)
+    dev = _check_dev(x)
+    B, n = x.shape
+    lo, hi = _taps(dec_lo), _taps(dec_hi)
+    w = torch.empty((B, level + 1, n), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_modwt", _ptr(x), x.stride(0), B, n, lo.ctypes.data_as(VP),
+                  hi.ctypes.data_as(VP), lo.size, int(level), _ptr(w), _stream(dev))
+    return w
+
+
+def imodwt(w: torch.Tensor, dec_lo, dec_hi, keep_mask: Optional[int] = None) -> torch.Tensor:
+    """[B, J + 1, n] -> [B, n]; rows with a clear bit in keep_mask count as zero."""
+    if w.dim() == 2:
+        w = w.unsqueeze(0)
+    w = w.to(torch.float32).contiguous()
+    dev = _check_dev(w)
+    B, R, n = w.shape
+    lo, hi = _taps(dec_lo), _taps(dec_hi)
+    keep = (1 << 64) - 1 if keep_mask is None else int(keep_mask)
+    x = torch.empty((B, n), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_imodwt", _ptr(w), B, n, lo.ctypes.data_as(VP), hi.ctypes.data_as(VP),
+                  lo.size, R - 1, C.c_ulonglong(keep), _ptr(x), x.stride(0), _stream(dev))
+    return x
+
+
+# ---------------------------------------------------------------------------- DWT
+def dwt_lengths(n: int, n_taps: int, level: int) -> list:
+    lens = (C.c_longlong * (level + 1))()
+    total = _lib.call("wtmi_dwt_lengths", n, n_taps, level, C.cast(lens, VP))
+    if total < 0:
+        raise ValueError("invalid DWT geometry")
+    return list(lens)
+
+
+def wavedec(x: torch.Tensor, dec_lo, dec_hi, level: int):
+    """Returns (coeffs [B, total] float32 in pywt order, lens)."""
+    x = _rows(x).to(torch.float32)
+    dev = _check_dev(x)
+    B, n = x.shape
+    lo, hi = _taps(dec_lo), _taps(dec_hi)
+    lens = dwt_lengths(n, lo.size, level)
+    coeffs = torch.empty((B, sum(lens)), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_wavedec", _ptr(x), x.stride(0), B, n, lo.ctypes.data_as(VP),
+                  hi.ctypes.data_as(VP), lo.size, int(level), _ptr(coeffs), _stream(dev))
+    return coeffs, lens
+
+
+def waverec(coeffs: torch.Tensor, n: int, rec_lo, rec_hi, level: int,
+            keep_masks: Sequence[int]) -> torch.Tensor:
+    """[B, total] -> [B, V, out_len]: one reconstruction per keep mask (bit k keeps
+    list entry k of [cA_J, cD_J, ..., cD_1])."""
+    if coeffs.dim() == 1:
+        coeffs = coeffs.unsqueeze(0)
+    coeffs = coeffs.to(torch.float32).contiguous()
+    dev = _check_dev(coeffs)
+    lo, hi = _taps(rec_lo), _taps(rec_hi)
+    lens = dwt_lengths(n, lo.size, level)
+    out_len = 2 * lens[-1] - lo.size + 2 if level > 0 else n
+    masks = torch.as_tensor(np.asarray([int(m) & ((1 << 64) - 1) for m in keep_masks],
+                                       dtype=np.uint64).view(np.int64), device=dev)
+    B = coeffs.shape[0]
+    out = torch.empty((B, len(keep_masks), out_len), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_waverec", _ptr(coeffs), B, n, lo.ctypes.data_as(VP),
+                  hi.ctypes.data_as(VP), lo.size, int(level), _ptr(masks), len(keep_masks),
+                  _ptr(out), out_len, _stream(dev))
+    return out

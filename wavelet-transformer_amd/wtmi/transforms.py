@@ -1,0 +1,361 @@
+"""pycwt / PyWavelets-shaped transforms on the MI355X engine (NumPy in, NumPy out).
+
+These are the functions the reference's wrapper modules call on third-party
+libraries -- ``pycwt.cwt / xwt / wct / ar1 / significance`` and ``pywt.wavedec /
+waverec / dwt_max_level`` -- re-provided over the HIP kernels in ``ops``.  Every
+[scales x time] array is produced on the GPU; the host only evaluates O(S) / O(n)
+closed forms (scales, periods, cone of influence, AR(1) spectra) exactly as the
+reference's libraries do.  Without a GPU every entry point raises.
+
+Batched device-tensor variants (``*_batch``) take ``[batch, n]`` torch tensors and
+return device tensors; the single-series functions wrap them.
+"""
+
+from __future__ import annotations
+
+import math
+import threading
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import ops
+from .wavelets import Morlet, as_filter_bank, as_morlet
+
+_dev_lock = threading.Lock()
+
+
+def device() -> torch.device:
+    """The GPU the NumPy-facing functions run on (current HIP device)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("wtmi needs an MI355X GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU implementation")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _to_dev(y, dtype=torch.float64) -> torch.Tensor:
+    if isinstance(y, torch.Tensor):
+        return y.to(device=device() if not y.is_cuda else y.device, dtype=dtype)
+    return torch.as_tensor(np.asarray(y), device=device()).to(dtype)
+
+
+def _np(t: torch.Tensor, dtype=None) -> np.ndarray:
+    a = t.detach().cpu().numpy()
+    return a.astype(dtype, copy=False) if dtype is not None else a
+
+
+# ------------------------------------------------------------------ closed forms
+def scales_for(n0: int, dt: float, dj: float, s0: float, J: float, wavelet: Morlet):
+    """pycwt ``cwt`` default resolution: s0 = 2 dt / lambda, J = round(log2(n0 dt / s0) / dj)."""
+    if s0 == -1:
+        s0 = 2 * dt / wavelet.flambda()
+    if J == -1:
+        J = int(np.round(np.log2(n0 * dt / s0) / dj))
+    sj = s0 * 2 ** (np.arange(0, J + 1) * dj)
+    freqs = 1 / (wavelet.flambda() * sj)
+    return sj, freqs
+
+
+def cone_of_influence(n0: int, dt: float, wavelet: Morlet) -> np.ndarray:
+    coi = n0 / 2 - np.abs(np.arange(0, n0) - (n0 - 1) / 2)
+    return wavelet.flambda() * wavelet.coi() * dt * coi
+
+
+def chi2_ppf_dof2(p: float) -> float:
+    """chi2.ppf(p, 2) = -2 ln(1 - p) (the only dof the Morlet path uses: dofmin = 2)."""
+    return -2.0 * math.log1p(-p)
+
+
+def _chi2_ppf(p: float, dof: int) -> float:
+    if dof == 2:
+        return chi2_ppf_dof2(p)
+    from scipy.stats import chi2  # only for non-Morlet dofs
+    return float(chi2.ppf(p, dof))
+
+
+def ar1_spectrum(freqs, ar1=0.0):
+    freqs = np.asarray(freqs)
+    return (1 - ar1 ** 2) / np.abs(1 - ar1 * np.exp(-2 * np.pi * 1j * freqs)) ** 2
+
+
+def _ar1_from_moments(c0: float, c1: float, N: int):
+    """pycwt ar1 after the lag-0/lag-1 covariances."""
+    B = -c1 * N - c0 * N ** 2 - 2 * c0 + 2 * c1 - c1 * N ** 2 + c0 * N
+    A = c0 * N ** 2
+    Cc = N * (c0 + c1 * N - c1)
+    D = B ** 2 - 4 * A * Cc
+    if D > 0:
+        g = (-B - D ** 0.5) / (2 * A)
+    else:
+        raise Warning("Cannot place an upperbound on the unbiased AR(1). "
+                      "Series is too short or trend is to large.")
+    mu2 = -1 / N + (2 / N ** 2) * ((N - g ** N) / (1 - g) - g * (1 - g ** (N - 1)) / (1 - g) ** 2)
+    c0t_pos = c0 / (1 - mu2)
+    a = ((1 - g ** 2) * c0t_pos) ** 0.5
+    return g, a, mu2
+
+
+def ar1(x):
+    """Unbiased AR(1) (g, a, mu2); covariances reduced on the GPU in fp64.
+    Raises the built-in ``Warning`` like pycwt (the app's CPI fallback relies on it)."""
+    xd = _to_dev(x)
+    m = _np(ops.series_moments(xd.reshape(1, -1)))[0]
+    return _ar1_from_moments(float(m[4]), float(m[5]), int(m[6]))
+
+
+def significance(signal, dt, scales, sigma_test=0, alpha=None, significance_level=0.95,
+                 dof=-1, wavelet="morlet"):
+    """pycwt ``significance`` for sigma_test == 0 (the only form the reference uses)."""
+    wavelet = as_morlet(wavelet)
+    try:
+        n0 = len(signal)
+    except TypeError:
+        n0 = 1
+    if n0 == 1:
+        variance = signal
+    else:
+        m = _np(ops.series_moments(_to_dev(signal).reshape(1, -1)))[0]
+        variance = m[1] ** 2
+    if alpha is None:
+        alpha, _, _ = ar1(signal)
+    if sigma_test != 0:
+        raise NotImplementedError("sigma_test != 0 is not used by the reference")
+    period = np.asarray(scales) * wavelet.flambda()
+    freq = dt / period
+    fft_theor = variance * (1 - alpha ** 2) / (1 + alpha ** 2 - 2 * alpha * np.cos(2 * np.pi * freq))
+    dof = wavelet.dofmin
+    signif = fft_theor * _chi2_ppf(significance_level, dof) / dof
+    return signif, fft_theor
+
+
+# ------------------------------------------------------------- standardisation
+def standardize_coefs(mom: torch.Tensor, detrend=True, standardize=True, remove_mean=False):
+    """[B,3] affine coefficients reproducing ``standardize_series`` from [B,8] moments."""
+    if detrend and remove_mean:
+        raise ValueError("Only standardize by either removing secular trend or mean, not both.")
+    B = mom.shape[0]
+    coef = torch.zeros((B, 3), dtype=torch.float64, device=mom.device)
+    if detrend:
+        coef[:, 0] = mom[:, 3]
+        coef[:, 1] = mom[:, 2]
+    elif remove_mean:
+        coef[:, 0] = mom[:, 0]
+    coef[:, 2] = 1.0 / mom[:, 1] if standardize else 1.0
+    return coef
+
+
+def normalize_coefs(mom: torch.Tensor) -> torch.Tensor:
+    """pycwt xwt/wct normalisation (y - mean) / std."""
+    coef = torch.zeros((mom.shape[0], 3), dtype=torch.float64, device=mom.device)
+    coef[:, 0] = mom[:, 0]
+    coef[:, 2] = 1.0 / mom[:, 1]
+    return coef
+
+
+def standardize_series_dev(y: torch.Tensor, detrend=True, standardize=True, remove_mean=False,
+                           dtype=torch.float64) -> torch.Tensor:
+    y = y if y.dim() == 2 else y.reshape(1, -1)
+    coef = standardize_coefs(ops.series_moments(y), detrend, standardize, remove_mean)
+    return ops.affine(y, coef, dtype)
+
+
+def standardize_series(series, detrend=True, standardize=True, remove_mean=False):
+    """GPU ``standardize_series`` (src/utils/wavelet_helpers.py:22-57), NumPy in/out."""
+    if detrend and remove_mean:
+        raise ValueError("Only standardize by either removing secular trend or mean, not both.")
+    s = np.asarray(series)
+    out = standardize_series_dev(_to_dev(s), detrend, standardize, remove_mean)
+    return _np(out)[0]
+
+
+# -------------------------------------------------------------------------- CWT
+def cwt_batch(x: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wavelet="morlet", *, affine=None,
+              sig_scale=None, want_w=True, want_power=False, want_sig=False):
+    """Batched Morlet CWT of device rows; returns (dict of device tensors, sj, freqs)."""
+    wavelet = as_morlet(wavelet)
+    n0 = x.shape[-1]
+    sj, freqs = scales_for(n0, dt, dj, s0, J, wavelet)
+    res = ops.cwt_morlet(x, sj, dt, wavelet.f0, affine=affine, sig_scale=sig_scale,
+                         want_w=want_w, want_power=want_power, want_sig=want_sig)
+    return res, sj, freqs
+
+
+def cwt(signal, dt, dj=1 / 12, s0=-1, J=-1, wavelet="morlet", freqs=None):
+    """pycwt-compatible ``cwt``: (W, sj, freqs, coi, signal_ft, ftfreqs)."""
+    wavelet = as_morlet(wavelet)
+    sig = np.asarray(signal)
+    n0 = sig.size
+    if freqs is not None:
+        freqs = np.asarray(freqs, dtype=float)
+        sj = 1 / (wavelet.flambda() * freqs)
+    else:
+        sj, freqs = scales_for(n0, dt, dj, s0, J, wavelet)
+    xd = _to_dev(sig).reshape(1, -1)
+    x32 = ops.affine(xd, torch.tensor([[0.0, 0.0, 1.0]], dtype=torch.float64, device=xd.device),
+                     torch.float32)
+    W = ops.cwt_morlet(x32, sj, dt, wavelet.f0, want_w=True)["w"][0]
+    N = int(2 ** np.ceil(np.log2(n0)))
+    ft = torch.fft.fft(xd[0], n=N)
+    ftfreqs = 2 * np.pi * np.fft.fftfreq(N, dt)
+    return (_np(W, np.complex128), sj, freqs, cone_of_influence(n0, dt, wavelet),
+            _np(ft[1:N // 2]) / N ** 0.5, ftfreqs[1:N // 2] / (2 * np.pi))
+
+
+# ----------------------------------------------------------------- XWT / WCT
+def _pair_norm(y1, y2):
+    d1, d2 = _to_dev(y1).reshape(1, -1), _to_dev(y2).reshape(1, -1)
+    m1, m2 = ops.series_moments(d1), ops.series_moments(d2)
+    return d1, d2, m1, m2
+
+
+def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95, wavelet="morlet",
+        normalize=True):
+    """pycwt-compatible ``xwt``: (W12, coi, freq, signif)."""
+    wavelet = as_morlet(wavelet)
+    d1, d2, m1, m2 = _pair_norm(y1, y2)
+    n0 = d1.shape[1]
+    sj, freq = scales_for(n0, dt, dj, s0, J, wavelet)
+    if normalize:
+        a1, a2 = normalize_coefs(m1), normalize_coefs(m2)
+    else:
+        ident = torch.tensor([[0.0, 0.0, 1.0]], dtype=torch.float64, device=d1.device)
+        a1 = a2 = ident
+    x1 = ops.affine(d1, a1, torch.float32)
+    x2 = ops.affine(d2, a2, torch.float32)
+    W12 = ops.xwt_morlet(x1, x2, sj, dt, wavelet.f0, want_w12=True)["w12"][0]
+    mh1, mh2 = _np(m1)[0], _np(m2)[0]
+    std1, std2 = (1.0, 1.0) if normalize else (mh1[1], mh2[1])
+    g1, _, _ = _ar1_from_moments(mh1[4], mh1[5], int(mh1[6]))
+    g2, _, _ = _ar1_from_moments(mh2[4], mh2[5], int(mh2[6]))
+    Pk1 = ar1_spectrum(freq * dt, g1)
+    Pk2 = ar1_spectrum(freq * dt, g2)
+    dof = wavelet.dofmin
+    signif = std1 * std2 * (Pk1 * Pk2) ** 0.5 * _chi2_ppf(significance_level, dof) / dof
+    return _np(W12, np.complex128), cone_of_influence(n0, dt, wavelet), freq, signif
+
+
+def boxcar_rows(wavelet: Morlet, dj: float) -> int:
+    """Morlet.smooth scale window length: int(round(2 * deltaj0 / dj))."""
+    return int(np.round(wavelet.deltaj0 / dj * 2))
+
+
+def wct_batch(y1: torch.Tensor, y2: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wavelet="morlet",
+              normalize=True, want_uv=True, workspace=None):
+    """Batched coherence of device row pairs: (dict coh/u/v, sj, freqs)."""
+    wavelet = as_morlet(wavelet)
+    if wavelet.deltaj0 <= 0:
+        raise ValueError("smoothing needs a Morlet(6) wavelet (deltaj0 defined)")
+    n0 = y1.shape[-1]
+    sj, freqs = scales_for(n0, dt, dj, s0, J, wavelet)
+    a1 = a2 = None
+    if normalize:
+        a1 = normalize_coefs(ops.series_moments(y1))
+        a2 = normalize_coefs(ops.series_moments(y2))
+    res = ops.wct_morlet(y1, y2, sj, dt, wavelet.f0, boxcar=boxcar_rows(wavelet, dj), affine1=a1,
+                         affine2=a2, want_uv=want_uv, workspace=workspace)
+    return res, sj, freqs
+
+
+def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
+        wavelet="morlet", normalize=True, **kwargs):
+    """pycwt-compatible ``wct``: (WCT, aWCT, coi, freq, sig); ``**kwargs`` are swallowed
+    as in pycwt (``cache=``, and ``delta_j=`` -- reference quirk B.5)."""
+    wavelet = as_morlet(wavelet)
+    if np.asarray(y1).size != np.asarray(y2).size:
+        raise AssertionError("Input signals must have the same size")
+    if sig:
+        raise NotImplementedError(
+            "wct(sig=True): the Monte-Carlo wct_significance is SURVEY 8(f) row 1 and not "
+            "implemented yet; call with sig=False")
+    d1, d2 = _to_dev(y1).reshape(1, -1), _to_dev(y2).reshape(1, -1)
+    x1 = _norm32(d1) if normalize else d1.to(torch.float32)
+    x2 = _norm32(d2) if normalize else d2.to(torch.float32)
+    res, sj, freq = wct_batch(x1, x2, dt, dj, s0, J, wavelet, normalize=False, want_uv=True)
+    u, v = res["u"][0], res["v"][0]
+    aWCT = torch.atan2(u, v)
+    n0 = d1.shape[1]
+    return (_np(res["coh"][0], np.float64), _np(aWCT, np.float64),
+            cone_of_influence(n0, dt, wavelet), freq, np.asarray([0]))
+
+
+def _norm32(d: torch.Tensor) -> torch.Tensor:
+    """(y - mean) / std in fp64 on the device, rounded once to fp32."""
+    return ops.affine(d, normalize_coefs(ops.series_moments(d)), torch.float32)
+
+
+# ------------------------------------------------------------------------- DWT
+def dwt_max_level(data_len: int, filter_len) -> int:
+    if not isinstance(filter_len, (int, np.integer)):
+        filter_len = as_filter_bank(filter_len).dec_len
+    if filter_len < 2:
+        raise ValueError("invalid wavelet filter length")
+    if data_len < filter_len - 1:
+        return 0
+    return int(np.floor(np.log2(data_len / (filter_len - 1))))
+
+
+def wavedec(data, wavelet, mode="symmetric", level=None):
+    """pywt-compatible ``wavedec`` (mode 'symmetric' only): [cA_n, cD_n, ..., cD_1]."""
+    if mode != "symmetric":
+        raise ValueError("only mode='symmetric' (the reference's) is implemented")
+    w = as_filter_bank(wavelet)
+    x = np.asarray(data)
+    if level is None:
+        level = dwt_max_level(x.size, w.dec_len)
+    if level < 0:
+        raise ValueError(f"Level value of {level} is too low . Minimum level is 0.")
+    xd = _to_dev(x, torch.float32).reshape(1, -1)
+    coeffs, lens = ops.wavedec(xd, w.dec_lo, w.dec_hi, level)
+    flat = _np(coeffs[0], np.float64)
+    out, off = [], 0
+    for L in lens:
+        out.append(flat[off:off + L])
+        off += L
+    return out
+
+
+def _pack_coeffs(coeffs, dec_len):
+    arrs = [np.asarray(c, dtype=np.float64) for c in coeffs]
+    level = len(arrs) - 1
+    # recover n from the finest detail length: len(cD_1) = (n + F - 1) // 2
+    # (n is ambiguous by one; the synthesis only needs the list lengths, which the
+    # kernel re-derives from n -- pick the n that reproduces every length)
+    d1 = arrs[-1].size if level > 0 else arrs[0].size
+    for n in ((2 * d1 - dec_len + 1, 2 * d1 - dec_len + 2) if level > 0 else (d1,)):
+        if n < 1:
+            continue
+        if ops.dwt_lengths(n, dec_len, level) == [a.size for a in arrs]:
+            return np.concatenate(arrs), n, level
+    raise ValueError("coefficient shape mismatch")
+
+
+def waverec_variants(coeffs, wavelet, keep_masks):
+    """Batched waverec: one reconstruction per keep mask (bit k keeps coeffs[k])."""
+    w = as_filter_bank(wavelet)
+    flat, n, level = _pack_coeffs(coeffs, w.dec_len)
+    dev = device()
+    ct = torch.as_tensor(flat.astype(np.float32), device=dev).reshape(1, -1)
+    out = ops.waverec(ct, n, w.rec_lo, w.rec_hi, level, keep_masks)
+    return _np(out[0], np.float64)
+
+
+def waverec(coeffs, wavelet, mode="symmetric"):
+    if mode != "symmetric":
+        raise ValueError("only mode='symmetric' (the reference's) is implemented")
+    return waverec_variants(coeffs, wavelet, [(1 << len(coeffs)) - 1])[0]
+
+
+# ----------------------------------------------------------------------- MODWT
+def modwt(x, wavelet, level):
+    w = as_filter_bank(wavelet)
+    a = np.asarray(x)
+    out = ops.modwt(_to_dev(a, torch.float32).reshape(1, -1), w.dec_lo, w.dec_hi, int(level))
+    return _np(out[0], a.dtype if a.dtype in (np.float32, np.float64) else np.float64)
+
+
+def imodwt(wc, wavelet, keep_mask=None):
+    w = as_filter_bank(wavelet)
+    a = np.asarray(wc)
+    out = ops.imodwt(_to_dev(a, torch.float32).unsqueeze(0), w.dec_lo, w.dec_hi, keep_mask)
+    return _np(out[0], a.dtype if a.dtype in (np.float32, np.float64) else np.float64)
