@@ -21,7 +21,10 @@ for s in $STEPS; do
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     tests) step pytest_gpu 1500 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} ; [ $? -le 1 ] || exit 1 ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} || exit $? ;;
-    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} || exit $? ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} || exit $? ;;
+    sweep) step sweep 600 python scripts/cwt_sweep.py || exit $? ;;
+    c3|c4|c5) step bench_$s 600 python bench.py --config $s --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
+    profall) step profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profall -o run -- python scripts/profile_all.py || exit $? ;;
   esac
 done
 echo ALLDONE

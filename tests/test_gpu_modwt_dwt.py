@@ -25,11 +25,17 @@ def _ops():
 
 
 def _check_rows(got, ref):
+    """Per row: normwise <= TOL and elementwise <= TOL * max|row|.  Rows that vanish
+    analytically (e.g. dilation = 0 mod N, where the taps sum to 0) hold only fp
+    round-off in either implementation, so every row also gets an absolute floor of
+    TOL * 1e-1 * the largest row max (documented in DESIGN.md)."""
     assert got.shape == ref.shape
-    err = row_relerr(got.astype(np.float64), ref.astype(np.float64))
-    assert err.max() <= TOL, err.max()
+    floor = 0.1 * TOL * np.abs(ref).max()
+    num = np.linalg.norm((got - ref).reshape(-1, ref.shape[-1]).astype(np.float64), axis=-1)
+    den = np.linalg.norm(ref.reshape(-1, ref.shape[-1]).astype(np.float64), axis=-1)
+    assert (num <= TOL * den + floor * np.sqrt(ref.shape[-1])).all(), (num / np.maximum(den, 1e-300)).max()
     scale = np.abs(ref).max(axis=-1, keepdims=True)
-    assert (np.abs(got - ref) <= TOL * scale + 1e-30).all()
+    assert (np.abs(got - ref) <= TOL * scale + floor).all()
 
 
 def test_modwt_matches_reference_golden(modwt_golden, db4):

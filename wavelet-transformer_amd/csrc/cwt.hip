@@ -60,8 +60,11 @@ template <int LOGN, int NBUF, int MODE>
 __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 : CwtGeom<LOGN, MODE>::MINW)) cwt_morlet_kernel(CwtArgs a) {
   using P = FftPlan<LOGN>;
   using G = CwtGeom<LOGN, MODE>;
-  __shared__ float2 lds[NBUF * G::ROWS * P::PADN + kMaxChunk];
-  float2* prm_tab = lds + NBUF * G::ROWS * P::PADN;
+  // per-scale table (alpha, log2 c, 1/signif, -) in LDS: the scale loop must not issue
+  // global loads -- a load's vmcnt wait would also wait for every store of the
+  // previous row (loads and stores retire in order on the same counter).
+  __shared__ float2 lds[NBUF * G::ROWS * P::PADN + 2 * kMaxChunk];
+  float4* prm_tab = reinterpret_cast<float4*>(lds + NBUF * G::ROWS * P::PADN);
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = tid - g * P::NT;
@@ -73,7 +76,11 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
   float2* my = lds + g * P::PADN;
   constexpr int bufstride = G::ROWS * P::PADN;
 
-  for (int i = tid; i < j1 - j0; i += G::BLOCK) prm_tab[i] = morlet_params(a.scales[j0 + i], a.dt, P::N);
+  for (int i = tid; i < j1 - j0; i += G::BLOCK) {
+    const float2 mp = morlet_params(a.scales[j0 + i], a.dt, P::N);
+    const float sg = a.sigscale ? static_cast<float>(a.sigscale[j0 + i]) : 0.f;
+    prm_tab[i] = make_float4(mp.x, mp.y, sg, 0.f);
+  }
 
   float2 tw[P::NTW_ALLOC];
   fft_twiddles<LOGN>(tw, t);
@@ -97,7 +104,8 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
   for (int it = 0; it < iters; ++it) {
     const int jl = it * G::ROWS + g;
     const bool valid = jl < j1 - j0;
-    const float2 prm = prm_tab[valid ? jl : 0];
+    const float4 prm4 = prm_tab[valid ? jl : 0];
+    const float2 prm = make_float2(prm4.x, prm4.y);
     float2 v[16];
     morlet_filter<LOGN>(v, X, prm, f0, t);
     fft_row<LOGN, 1, NBUF>(v, my, bufstride, tw, t, par);
@@ -113,7 +121,7 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
     if (!valid) continue;
     const int j = j0 + jl;
     const long long rowbase = (b * a.S + j) * static_cast<long long>(a.n0);
-    const float sg = a.sigscale ? static_cast<float>(a.sigscale[j]) : 0.f;
+    const float sg = prm4.z;
     if (full)
       store_any<LOGN, true>(v, a, kind, rowbase, sg, t);
     else
