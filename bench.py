@@ -215,14 +215,14 @@ class C4:
         self.bytes = self.units * 12 + self.P * self.n * 8
         self.ws = torch.empty(ops.wct_workspace_bytes(self.P, self.n, S), dtype=torch.uint8,
                               device=dev)
-        self.kernel = "wct_phase_a<13>+wct_phase_b<10>+xwt"
+        self.kernel = "wct_spectra<13>+wct_phase_a<13>+wct_phase_b<10>"
         self.unit_name = "coeffs/s"
-        self.bytes_note = "12 B/coeff (|W12|^2, WCT, phase) + 8 B/pair-sample inputs"
+        self.bytes_note = "12 B/coeff (|W12|^2 + WCT + phase, f32) + 8 B/pair-sample inputs"
 
     def step(self):
+        # one fused pass: XWT power |W1 W2*|^2, phase angle and WCT coherence
         self.r = self.T.wct_batch(self.y1, self.y2, DT, self.dj, 2 * DT, -1, workspace=self.ws,
-                                  want_uv=True)[0]
-        self.p = self.ops.xwt_morlet(self.y1, self.y2, self.sj, DT, want_power=True)
+                                  want_uv=False, want_power=True, want_phase=True)[0]
 
     def check(self):
         c = self.r["coh"]
@@ -240,8 +240,8 @@ CONFIGS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--cpu-per-worker", type=int, default=32)

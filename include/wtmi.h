@@ -53,17 +53,19 @@ int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long ba
                     const double* sig_scale, float* out_w12, float* out_power, float* out_sig,
                     float* out_u, float* out_v, void* stream);
 
-/* ---- WCT coherence (K1+K2+K7+K8) ---------------------------------------------
+/* ---- WCT coherence + XWT power / phase (K1+K2+K7+K8) ---------------------------
  * Replaces pycwt.wct(..., sig=False) numerics (src/wct.py:106-118): two CWTs,
  * Morlet.smooth of |W1|^2/s, |W2|^2/s, W12/s (time Gaussian via FFT + scale boxcar of
- * `boxcar` rows), WCT = |S12|^2/(S1 S2) and the phase arrows of angle(W12).
+ * `boxcar` rows), WCT = |S12|^2/(S1 S2), aWCT = angle(W12) and the phase arrows; the
+ * same pass emits the cross-wavelet power |W1 W2*|^2 (pycwt.xwt, src/xwt.py:93).
  * workspace: device scratch of wtmi_wct_workspace_bytes(batch, n0, n_scales) bytes.
- * Outputs (out_u/out_v may be NULL): coherence, u, v [batch][n_scales][n0] float32. */
+ * Outputs [batch][n_scales][n0] float32; all but out_coh may be NULL (u, v together). */
 long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales);
 int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch, long long n0,
                     const double* affine1, const double* affine2, const double* scales,
                     int n_scales, double dt, double f0, int boxcar, void* workspace,
-                    float* out_coh, float* out_u, float* out_v, void* stream);
+                    float* out_coh, float* out_power, float* out_phase, float* out_u,
+                    float* out_v, void* stream);
 
 /* ---- MODWT (K3 / K4) -----------------------------------------------------------
  * Replace src/modwt.py:126-144 (modwt: rows [W_1..W_J, V_J]) and :147-160 (imodwt).

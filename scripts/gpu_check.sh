@@ -23,6 +23,17 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} || exit $? ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} || exit $? ;;
     sweep) step sweep 600 python scripts/cwt_sweep.py || exit $? ;;
+    diag)  step diag 600 python scripts/cwt_diag.py --mode seq || exit $? ;;
+    counters) step counters 300 rocprofv3 -L ;;
+    pmc)
+      i=0
+      GROUPS_STR=${PMC_GROUPS:-"WRITE_SIZE;FETCH_SIZE;GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES;SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY;SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU"}
+      IFS=';' read -ra GRPS <<< "$GROUPS_STR"
+      for grp in "${GRPS[@]}"; do
+        i=$((i+1))
+        step pmc$i 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/pmc$i -o run -- python ${PMC_SCRIPT:-scripts/cwt_diag.py} --mode short
+        rc=$?; [ $rc -ge 124 ] && exit $rc
+      done ;;
     c3|c4|c5) step bench_$s 600 python bench.py --config $s --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
     profall) step profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profall -o run -- python scripts/profile_all.py || exit $? ;;
   esac

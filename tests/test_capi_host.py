@@ -113,3 +113,13 @@ def test_gpu_entry_points_fail_loudly_without_gpu():
     from wtmi import ops
     with pytest.raises(RuntimeError, match="GPU"):
         ops.cwt_morlet(torch.zeros(2, 32), [1.0], 1.0)
+
+
+def test_torch_custom_ops_registered_and_gpu_only():
+    import torch
+    import wtmi.ops  # noqa: F401
+    for name in ("cwt", "cwt_power", "wct", "modwt", "imodwt"):
+        assert hasattr(torch.ops.wtmi, name)
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError, match="GPU"):
+            torch.ops.wtmi.cwt(torch.zeros(1, 32), torch.ones(3, dtype=torch.float64), 1.0, 6.0)

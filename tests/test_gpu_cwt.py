@@ -114,3 +114,23 @@ def test_rejects_cpu_tensors_and_bad_args():
     with pytest.raises(_lib.WtmiError):
         _lib.call("wtmi_cwt_morlet", None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, None, None,
                   None, None)
+
+
+def test_torch_custom_ops_match_oracle(db4):
+    import wtmi.ops  # noqa: F401  (registers torch.ops.wtmi)
+    from oracle import modwt_spec as ms
+    rng = np.random.default_rng(21)
+    n0, dt = 512, 1 / 12
+    x = np.stack([red_series(rng, n0) for _ in range(2)])
+    sj = _scales(n0, dt, 1 / 8, 2 * dt, 40)
+    xd = torch.tensor(x, device="cuda")
+    W = torch.ops.wtmi.cwt(xd, torch.tensor(sj, device="cuda"), dt, 6.0).cpu().numpy()
+    ref = pc.cwt(x[1].astype(np.float64), dt, 1 / 8, 2 * dt, 40)[0]
+    assert row_relerr(W[1].astype(np.complex128), ref).max() < TOL
+    lo = torch.tensor(db4["dec_lo"])
+    hi = torch.tensor(db4["dec_hi"])
+    w = torch.ops.wtmi.modwt(xd, lo, hi, 4)
+    r = ms.modwt(x[0].astype(np.float64), db4["dec_lo"], db4["dec_hi"], 4)
+    assert np.abs(w[0].cpu().numpy() - r).max() <= 1e-5 * np.abs(r).max()
+    xr = torch.ops.wtmi.imodwt(w, lo, hi).cpu().numpy()
+    assert np.abs(xr - x).max() <= 1e-5 * np.abs(x).max()

@@ -51,6 +51,32 @@ def test_wct_matches_oracle(n, dj):
     np.testing.assert_allclose(freq, rfreq, rtol=1e-12)
 
 
+def test_wct_fused_power_and_phase_outputs():
+    from wtmi import ops, transforms
+    rng = np.random.default_rng(31)
+    n, B = 1000, 3
+    pairs = [_pair(rng, n) for _ in range(B)]
+    y1 = torch.tensor(np.stack([p[0] for p in pairs]), device="cuda", dtype=torch.float32)
+    y2 = torch.tensor(np.stack([p[1] for p in pairs]), device="cuda", dtype=torch.float32)
+    res, sj, _ = transforms.wct_batch(y1, y2, 1 / 12, 1 / 8, 2 / 12, -1, want_uv=True,
+                                      want_power=True, want_phase=True)
+    for b in range(B):
+        a1 = y1[b].cpu().numpy().astype(np.float64)
+        a2 = y2[b].cpu().numpy().astype(np.float64)
+        W12 = (pc.cwt((a1 - a1.mean()) / a1.std(), 1 / 12, 1 / 8, 2 / 12, -1)[0]
+               * pc.cwt((a2 - a2.mean()) / a2.std(), 1 / 12, 1 / 8, 2 / 12, -1)[0].conj())
+        p = res["power"][b].cpu().numpy().astype(np.float64)
+        assert row_relerr(p, np.abs(W12) ** 2).max() < 5e-5
+        mask = np.abs(W12) > 1e-3 * np.abs(W12).max()
+        ph = res["phase"][b].cpu().numpy()
+        assert np.abs(np.angle(np.exp(1j * (ph - np.angle(W12))))[mask]).max() < 1e-4
+        u, v = res["u"][b].cpu().numpy(), res["v"][b].cpu().numpy()
+        np.testing.assert_allclose(u[mask], np.sin(ph[mask]), atol=1e-5)
+        np.testing.assert_allclose(v[mask], np.cos(ph[mask]), atol=1e-5)
+        rc = pc.wct(a1, a2, 1 / 12, dj=1 / 8, s0=2 / 12, J=-1, sig=False)[0]
+        assert np.abs(res["coh"][b].cpu().numpy() - rc).max() <= 1e-4
+
+
 def test_wct_batched_self_coherence_is_one():
     from wtmi import transforms
     rng = np.random.default_rng(2)

@@ -17,10 +17,10 @@ namespace wtmi {
 enum : int { kOutW = 1, kOutPow = 2, kOutSig = 4, kOutUV = 8 };
 
 template <int LOGN, int KIND, bool FULL>
-__device__ __forceinline__ void store_row(const float2 (&v)[16], const CwtArgs& a, long long rowbase,
+__device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, long long rowbase,
                                           float sg, int t) {
   using P = FftPlan<LOGN>;
-  float2* pw_ = (KIND & kOutW) ? a.out_w + rowbase : nullptr;
+  cpx* pw_ = (KIND & kOutW) ? a.out_w + rowbase : nullptr;
   float* pp_ = (KIND & kOutPow) ? a.out_pow + rowbase : nullptr;
   float* ps_ = (KIND & kOutSig) ? a.out_sig + rowbase : nullptr;
   float* pu_ = (KIND & kOutUV) ? a.out_u + rowbase : nullptr;
@@ -43,7 +43,7 @@ __device__ __forceinline__ void store_row(const float2 (&v)[16], const CwtArgs& 
 }
 
 template <int LOGN, bool FULL>
-__device__ __forceinline__ void store_any(const float2 (&v)[16], const CwtArgs& a, int kind,
+__device__ __forceinline__ void store_any(const cpx (&v)[16], const CwtArgs& a, int kind,
                                           long long rowbase, float sg, int t) {
   switch (kind) {
 #define WTMI_K(K) case K: store_row<LOGN, K, FULL>(v, a, rowbase, sg, t); break;
@@ -63,7 +63,7 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
   // per-scale table (alpha, log2 c, 1/signif, -) in LDS: the scale loop must not issue
   // global loads -- a load's vmcnt wait would also wait for every store of the
   // previous row (loads and stores retire in order on the same counter).
-  __shared__ float2 lds[NBUF * G::ROWS * P::PADN + 2 * kMaxChunk];
+  __shared__ cpx lds[NBUF * G::ROWS * P::PADN + 2 * kMaxChunk];
   float4* prm_tab = reinterpret_cast<float4*>(lds + NBUF * G::ROWS * P::PADN);
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
@@ -73,23 +73,23 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
   const int ch = static_cast<int>(blk - b * a.nchunks);
   const int j0 = ch * a.chunk;
   const int j1 = min(a.S, j0 + a.chunk);
-  float2* my = lds + g * P::PADN;
+  cpx* my = lds + g * P::PADN;
   constexpr int bufstride = G::ROWS * P::PADN;
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
-    const float2 mp = morlet_params(a.scales[j0 + i], a.dt, P::N);
+    const cpx mp = morlet_params(a.scales[j0 + i], a.dt, P::N);
     const float sg = a.sigscale ? static_cast<float>(a.sigscale[j0 + i]) : 0.f;
     prm_tab[i] = make_float4(mp.x, mp.y, sg, 0.f);
   }
 
-  float2 tw[P::NTW_ALLOC];
+  cpx tw[P::NTW_ALLOC];
   fft_twiddles<LOGN>(tw, t);
   int par = 0;
 
-  float2 X[16];
+  cpx X[16];
   load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
   fft_row<LOGN, -1, NBUF>(X, my, bufstride, tw, t, par);
-  float2 X2[MODE == 1 ? 16 : 1];
+  cpx X2[MODE == 1 ? 16 : 1];
   if constexpr (MODE == 1) {
     load_series<LOGN>(X2, a.x2, a.affine2, b, a.ld, a.n0, t);
     fft_row<LOGN, -1, NBUF>(X2, my, bufstride, tw, t, par);
@@ -105,12 +105,12 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
     const int jl = it * G::ROWS + g;
     const bool valid = jl < j1 - j0;
     const float4 prm4 = prm_tab[valid ? jl : 0];
-    const float2 prm = make_float2(prm4.x, prm4.y);
-    float2 v[16];
+    const cpx prm = mkc(prm4.x, prm4.y);
+    cpx v[16];
     morlet_filter<LOGN>(v, X, prm, f0, t);
     fft_row<LOGN, 1, NBUF>(v, my, bufstride, tw, t, par);
     if constexpr (MODE == 1) {
-      float2 w1[16];
+      cpx w1[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) w1[m] = v[m];
       morlet_filter<LOGN>(v, X2, prm, f0, t);
@@ -167,9 +167,9 @@ __global__ void __launch_bounds__(256) cwt_direct_kernel(CwtArgs a, int N) {
     }
     w[which] = make_double2(acc_re, acc_im);
   }
-  float2 v = make_float2(static_cast<float>(w[0].x), static_cast<float>(w[0].y));
+  cpx v = mkc(static_cast<float>(w[0].x), static_cast<float>(w[0].y));
   if constexpr (MODE == 1) {
-    const float2 w2 = make_float2(static_cast<float>(w[1].x), static_cast<float>(w[1].y));
+    const cpx w2 = mkc(static_cast<float>(w[1].x), static_cast<float>(w[1].y));
     v = cmul(v, cconj(w2));
   }
   const long long o = idx;
@@ -270,7 +270,7 @@ extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, lo
   a.dt = dt;
   a.f0 = f0;
   a.sigscale = sig_scale;
-  a.out_w = reinterpret_cast<float2*>(out_w);
+  a.out_w = reinterpret_cast<cpx*>(out_w);
   a.out_pow = out_power;
   a.out_sig = out_sig;
   return dispatch<0>(a, static_cast<hipStream_t>(stream));
@@ -299,7 +299,7 @@ extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, l
   a.dt = dt;
   a.f0 = f0;
   a.sigscale = sig_scale;
-  a.out_w = reinterpret_cast<float2*>(out_w12);
+  a.out_w = reinterpret_cast<cpx*>(out_w12);
   a.out_pow = out_power;
   a.out_sig = out_sig;
   a.out_u = out_u;

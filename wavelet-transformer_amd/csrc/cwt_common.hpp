@@ -18,7 +18,7 @@ struct CwtArgs {
   const double* scales;  // [S] device
   double dt, f0;
   const double* sigscale;  // [S] multiplier for the ratio output (1 / signif), or null
-  float2* out_w;
+  cpx* out_w;
   float* out_pow;
   float* out_sig;
   float* out_u;
@@ -41,7 +41,7 @@ struct CwtGeom {
 };
 
 template <int LOGN>
-__device__ __forceinline__ void load_series(float2 (&v)[16], const float* __restrict__ x,
+__device__ __forceinline__ void load_series(cpx (&v)[16], const float* __restrict__ x,
                                             const double* __restrict__ affine, long long b,
                                             long long ld, int n0, int t) {
   using P = FftPlan<LOGN>;
@@ -61,22 +61,22 @@ __device__ __forceinline__ void load_series(float2 (&v)[16], const float* __rest
       val = row[pos];
       if (aff) val = static_cast<float>((static_cast<double>(val) - a0 - a1 * pos) * a2);
     }
-    v[m] = make_float2(val, 0.f);
+    v[m] = mkc(val, 0.f);
   }
 }
 
 // Per-scale filter constants: e_k = alpha * kk - f0, psi_k = exp2(lc - log2(e)/2 * e_k^2)
 // with alpha = 2 pi s / (N dt) and 2^lc = sqrt(2 pi s / dt) * pi^-1/4 / N (1/N of the IFFT).
-__device__ __forceinline__ float2 morlet_params(double s, double dt, int N) {
+__device__ __forceinline__ cpx morlet_params(double s, double dt, int N) {
   const double alpha = s * 2.0 * kPi / (static_cast<double>(N) * dt);
   const double c = sqrt(2.0 * kPi * s / dt) * 0.75112554446494248286 / static_cast<double>(N);
-  return make_float2(static_cast<float>(alpha), static_cast<float>(log2(c)));
+  return mkc(static_cast<float>(alpha), static_cast<float>(log2(c)));
 }
 
 // v = X * psi_bar_j / N for the 16 bins this thread owns.  Bin k = t + m*NT has the
 // signed frequency index kk = t + (m < 8 ? m : m - 16) * NT (fftfreq ordering).
 template <int LOGN>
-__device__ __forceinline__ void morlet_filter(float2 (&v)[16], const float2 (&X)[16], float2 prm,
+__device__ __forceinline__ void morlet_filter(cpx (&v)[16], const cpx (&X)[16], cpx prm,
                                               float f0, int t) {
   using P = FftPlan<LOGN>;
   constexpr float K = -0.5f * kLog2e;

@@ -31,48 +31,50 @@ __host__ __device__ constexpr float cos16(int m) {
 __host__ __device__ constexpr float sin16(int m) { return cos16(m - 4); }
 
 template <int DIR>
-__device__ __forceinline__ float2 mul_i(float2 a) {  // a * (DIR * i)
-  return DIR > 0 ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+__device__ __forceinline__ cpx mul_i(cpx a) {  // a * (DIR * i)
+  return DIR > 0 ? a.yx * cpx{-1.f, 1.f} : a.yx * cpx{1.f, -1.f};
 }
 
 template <int DIR, int M>
-__device__ __forceinline__ float2 rot16(float2 a) {  // a * exp(DIR * 2 pi i M / 16)
+__device__ __forceinline__ cpx rot16(cpx a) {  // a * exp(DIR * 2 pi i M / 16)
   constexpr int m = M & 15;
   if constexpr (m == 0) {
     return a;
   } else if constexpr (m == 4) {
     return mul_i<DIR>(a);
   } else if constexpr (m == 8) {
-    return make_float2(-a.x, -a.y);
+    return mkc(-a.x, -a.y);
   } else if constexpr (m == 12) {
     return mul_i<-DIR>(a);
   } else {
     constexpr float c = cos16(m);
     constexpr float s = DIR * sin16(m);
-    return make_float2(fmaf(a.x, c, -a.y * s), fmaf(a.x, s, a.y * c));
+    return cfma(a.yy, cpx{-s, c}, a.xx * cpx{c, s});
   }
 }
 
 template <int DIR>
-__device__ __forceinline__ void dft2(float2& a, float2& b) {
-  const float2 t = a;
+__device__ __forceinline__ void dft2(cpx& a, cpx& b) {
+  const cpx t = a;
   a = cadd(t, b);
   b = csub(t, b);
 }
 
 template <int DIR>
-__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
-  const float2 t0 = cadd(x0, x2), t1 = csub(x0, x2);
-  const float2 t2 = cadd(x1, x3), t3 = mul_i<DIR>(csub(x1, x3));
-  x0 = cadd(t0, t2);
-  x2 = csub(t0, t2);
-  x1 = cadd(t1, t3);
-  x3 = csub(t1, t3);
+__device__ __forceinline__ void dft4(cpx& x0, cpx& x1, cpx& x2, cpx& x3) {
+  // X1 = t1 + DIR i d, X3 = t1 - DIR i d with d = x1 - x3: one packed fma each
+  const cpx t0 = x0 + x2, t1 = x0 - x2;
+  const cpx t2 = x1 + x3, d = x1 - x3;
+  constexpr float sd = static_cast<float>(DIR);
+  x0 = t0 + t2;
+  x2 = t0 - t2;
+  x1 = cfma(d.yx, cpx{-sd, sd}, t1);
+  x3 = cfma(d.yx, cpx{sd, -sd}, t1);
 }
 
 // 8-point DFT on v[0..7], natural order in and out (2 x 4 Cooley-Tukey).
 template <int DIR>
-__device__ __forceinline__ void dft8(float2* v) {
+__device__ __forceinline__ void dft8(cpx* v) {
 #pragma unroll
   for (int n2 = 0; n2 < 4; ++n2) dft2<DIR>(v[n2], v[n2 + 4]);
   v[5] = rot16<DIR, 2>(v[5]);
@@ -80,7 +82,7 @@ __device__ __forceinline__ void dft8(float2* v) {
   v[7] = rot16<DIR, 6>(v[7]);
   dft4<DIR>(v[0], v[1], v[2], v[3]);
   dft4<DIR>(v[4], v[5], v[6], v[7]);
-  float2 t[8];
+  cpx t[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) t[i] = v[i];
 #pragma unroll
@@ -91,7 +93,7 @@ __device__ __forceinline__ void dft8(float2* v) {
 
 // 16-point DFT on v[0..15], natural order in and out (4 x 4 Cooley-Tukey).
 template <int DIR>
-__device__ __forceinline__ void dft16(float2* v) {
+__device__ __forceinline__ void dft16(cpx* v) {
 #pragma unroll
   for (int n2 = 0; n2 < 4; ++n2) dft4<DIR>(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]);
   v[5] = rot16<DIR, 1>(v[5]);
@@ -105,7 +107,7 @@ __device__ __forceinline__ void dft16(float2* v) {
   v[15] = rot16<DIR, 9>(v[15]);
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) dft4<DIR>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
-  float2 t[16];
+  cpx t[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) t[i] = v[i];
 #pragma unroll
@@ -115,7 +117,7 @@ __device__ __forceinline__ void dft16(float2* v) {
 }
 
 template <int R, int DIR>
-__device__ __forceinline__ void dft_small(float2* v) {
+__device__ __forceinline__ void dft_small(cpx* v) {
   if constexpr (R == 2) {
     dft2<DIR>(v[0], v[1]);
   } else if constexpr (R == 4) {
@@ -146,16 +148,16 @@ struct FftPlan {
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
 // exp(+2 pi i num / den), correctly rounded from double.
-__device__ __forceinline__ float2 expi_frac(long long num, long long den) {
+__device__ __forceinline__ cpx expi_frac(long long num, long long den) {
   num %= den;
   double s, c;
   sincospi(2.0 * static_cast<double>(num) / static_cast<double>(den), &s, &c);
-  return make_float2(static_cast<float>(c), static_cast<float>(s));
+  return mkc(static_cast<float>(c), static_cast<float>(s));
 }
 
 // Per-thread base twiddles (inverse sign; the forward transform conjugates them).
 template <int LOGN>
-__device__ __forceinline__ void fft_twiddles(float2* tw, int t) {
+__device__ __forceinline__ void fft_twiddles(cpx* tw, int t) {
   using P = FftPlan<LOGN>;
   long long ns = 16;
 #pragma unroll
@@ -189,22 +191,22 @@ __device__ __forceinline__ void fft_twiddles(float2* tw, int t) {
 }
 
 template <int DIR>
-__device__ __forceinline__ float2 twd(float2 w) { return DIR > 0 ? w : cconj(w); }
+__device__ __forceinline__ cpx twd(cpx w) { return DIR > 0 ? w : cconj(w); }
 
 // Hide a value from loop-invariant code motion: keeps only the base twiddles live
 // across a caller's loop instead of all 15 derived powers (+ swapped copies for
 // packed math), which otherwise pushes the CWT kernel to 256 VGPRs.
-__device__ __forceinline__ float2 opaque(float2 w) {
+__device__ __forceinline__ cpx opaque(cpx w) {
   asm volatile("" : "+v"(w.x), "+v"(w.y));
   return w;
 }
 
 // v[r] *= w^r for r = 1..15 from the bases w, w^2, w^4, w^8.
 template <int DIR>
-__device__ __forceinline__ void apply_tw16(float2* v, const float2* b) {
-  const float2 w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
-  const float2 w4 = twd<DIR>(opaque(b[2])), w8 = twd<DIR>(opaque(b[3]));
-  const float2 w3 = cmul(w1, w2), w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
+__device__ __forceinline__ void apply_tw16(cpx* v, const cpx* b) {
+  const cpx w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
+  const cpx w4 = twd<DIR>(opaque(b[2])), w8 = twd<DIR>(opaque(b[3]));
+  const cpx w3 = cmul(w1, w2), w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
   v[1] = cmul(v[1], w1);
   v[2] = cmul(v[2], w2);
   v[3] = cmul(v[3], w3);
@@ -223,18 +225,18 @@ __device__ __forceinline__ void apply_tw16(float2* v, const float2* b) {
 }
 
 template <int R, int DIR>
-__device__ __forceinline__ void apply_tw_small(float2* v, const float2* b) {
+__device__ __forceinline__ void apply_tw_small(cpx* v, const cpx* b) {
   if constexpr (R == 2) {
     v[1] = cmul(v[1], twd<DIR>(b[0]));
   } else if constexpr (R == 4) {
-    const float2 w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
+    const cpx w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
     v[1] = cmul(v[1], w1);
     v[2] = cmul(v[2], w2);
     v[3] = cmul(v[3], cmul(w1, w2));
   } else {
-    const float2 w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
-    const float2 w4 = twd<DIR>(opaque(b[2]));
-    const float2 w3 = cmul(w1, w2);
+    const cpx w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
+    const cpx w4 = twd<DIR>(opaque(b[2]));
+    const cpx w3 = cmul(w1, w2);
     v[1] = cmul(v[1], w1);
     v[2] = cmul(v[2], w2);
     v[3] = cmul(v[3], w3);
@@ -246,21 +248,21 @@ __device__ __forceinline__ void apply_tw_small(float2* v, const float2* b) {
 }
 
 // In-place FFT of one row.  v[m] holds position t + m*NT on entry and exit.
-// lds: this row's region of buffer 0; bufstride: offset (in float2) of buffer 1
+// lds: this row's region of buffer 0; bufstride: offset (in cpx) of buffer 1
 // when NBUF == 2.  par: running buffer parity (NBUF == 2), shared by all calls of
 // the workgroup in the same order.  Every thread of the workgroup must call this
 // the same number of times (it contains __syncthreads()).
 template <int LOGN, int DIR, int NBUF>
-__device__ __forceinline__ void fft_row(float2 (&v)[16], float2* __restrict__ lds, int bufstride,
-                                        const float2* tw, int t, int& par) {
+__device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int bufstride,
+                                        const cpx* tw, int t, int& par) {
   using P = FftPlan<LOGN>;
   constexpr bool kAligned = (P::NT % 16) == 0;  // strides are multiples of 16 -> pad is additive
   dft16<DIR>(v);
   if constexpr (P::NPASS == 1) return;
   {
-    float2* buf = lds + (NBUF == 2 ? par * bufstride : 0);
+    cpx* buf = lds + (NBUF == 2 ? par * bufstride : 0);
     if constexpr (NBUF == 1) __syncthreads();
-    float2* w = buf + 17 * t;  // lpad(16 t + r) = 17 t + r
+    cpx* w = buf + 17 * t;  // lpad(16 t + r) = 17 t + r
 #pragma unroll
     for (int r = 0; r < 16; ++r) w[r] = v[r];
     __syncthreads();
@@ -270,10 +272,10 @@ __device__ __forceinline__ void fft_row(float2 (&v)[16], float2* __restrict__ ld
 #pragma unroll
   for (int p = 1; p < P::NPASS; ++p) {
     const bool last = (p == P::NPASS - 1);
-    const float2* rbuf = lds + (NBUF == 2 ? par * bufstride : 0);
+    const cpx* rbuf = lds + (NBUF == 2 ? par * bufstride : 0);
     if (p < P::P16) {
       if constexpr (kAligned) {
-        const float2* rb = rbuf + pt;
+        const cpx* rb = rbuf + pt;
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = rb[r * (P::NT + P::NT / 16)];
       } else {
@@ -284,10 +286,10 @@ __device__ __forceinline__ void fft_row(float2 (&v)[16], float2* __restrict__ ld
       apply_tw16<DIR>(v, tw + 4 * (p - 1));
       dft16<DIR>(v);
       if (!last) {
-        float2* wbuf = lds + (NBUF == 2 ? par * bufstride : 0);
+        cpx* wbuf = lds + (NBUF == 2 ? par * bufstride : 0);
         const int idxD = (t / ns) * ns * 16 + (t & (ns - 1));
         if constexpr (NBUF == 1) __syncthreads();
-        float2* wb = wbuf + lpad(idxD);  // ns >= 16 -> r*ns keeps the pad additive
+        cpx* wb = wbuf + lpad(idxD);  // ns >= 16 -> r*ns keeps the pad additive
 #pragma unroll
         for (int r = 0; r < 16; ++r) wb[r * (ns + ns / 16)] = v[r];
         __syncthreads();
@@ -316,7 +318,7 @@ __device__ __forceinline__ void fft_row(float2 (&v)[16], float2* __restrict__ ld
         dft_small<R, DIR>(v + q * R);
       }
       // register q*R + r holds position t + (q + r*Q)*NT
-      float2 o[16];
+      cpx o[16];
 #pragma unroll
       for (int q = 0; q < Q; ++q)
 #pragma unroll

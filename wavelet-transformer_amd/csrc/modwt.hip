@@ -213,6 +213,190 @@ __global__ void __launch_bounds__(1024) imodwt_kernel(const float* __restrict__ 
   for (int i = tid; i < n; i += T) xo[i] = V[i];
 }
 
+// ---------------------------------------------------------------------------------
+// Fast path: n % 4 == 0, L = 8 (db4, the reference's wavelet).  Threads own groups of
+// 4 consecutive samples (float4).  Levels j >= 3 have a dilation that is a multiple
+// of 4, so every tap is one aligned ds_read_b128; levels 1 and 2 read a register
+// window of 3 / 5 aligned float4 blocks and form all taps from it.
+constexpr int kVecGroups = 8;  // float4 groups per thread (n <= 4 * 8 * block)
+
+template <int L, int DM, bool FWD>
+__device__ __forceinline__ void window_taps(const float4* __restrict__ V4, int q, int ng,
+                                            const FilterBank& fb, float4& a, float4& b) {
+  // FWD: taps at p - DM*l (analysis); else p + DM*l (synthesis).  Window of NB blocks.
+  constexpr int SPAN = (L - 1) * DM;        // samples reached beyond the group
+  constexpr int NB = (SPAN + 3) / 4 + 1;    // aligned float4 blocks covering it
+  float f[4 * NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    int qs = FWD ? q - (NB - 1) + u : q + u;
+    qs = qs < 0 ? qs + ng : (qs >= ng ? qs - ng : qs);
+    const float4 v = V4[qs];
+    f[4 * u] = v.x; f[4 * u + 1] = v.y; f[4 * u + 2] = v.z; f[4 * u + 3] = v.w;
+  }
+  float ra[4] = {0.f, 0.f, 0.f, 0.f}, rb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const float hl = fb.h[l], gl = fb.g[l];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = FWD ? 4 * (NB - 1) + i - DM * l : i + DM * l;
+      ra[i] = fmaf(hl, f[idx], ra[i]);
+      rb[i] = fmaf(gl, f[idx], rb[i]);
+    }
+  }
+  a = make_float4(ra[0], ra[1], ra[2], ra[3]);
+  b = make_float4(rb[0], rb[1], rb[2], rb[3]);
+}
+
+__device__ __forceinline__ void fma4(float4& acc, float c, const float4& s) {
+  acc.x = fmaf(c, s.x, acc.x); acc.y = fmaf(c, s.y, acc.y);
+  acc.z = fmaf(c, s.z, acc.z); acc.w = fmaf(c, s.w, acc.w);
+}
+
+template <int L>
+__global__ void __launch_bounds__(512, 2) modwt_vec_kernel(const float* __restrict__ x, long long ld,
+                                                           int n, int level, FilterBank fb,
+                                                           float* __restrict__ w) {
+  extern __shared__ __attribute__((aligned(16))) float4 V4[];
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const long long b = blockIdx.x;
+  const int ng = n >> 2;
+  const float4* xin = reinterpret_cast<const float4*>(x + b * ld);
+  float* wout = w + b * static_cast<long long>(level + 1) * n;
+  for (int q = tid; q < ng; q += T) V4[q] = xin[q];
+  __syncthreads();
+  for (int j = 1; j <= level; ++j) {
+    const int dm = static_cast<int>((1ll << (j - 1)) % n);
+    float4* wrow = reinterpret_cast<float4*>(wout + static_cast<long long>(j - 1) * n);
+    float4 vreg[kVecGroups];
+#pragma unroll
+    for (int k = 0; k < kVecGroups; ++k) {
+      const int q = tid + k * T;
+      if (q < ng) {
+        float4 aw, av;
+        if (dm == 1) {
+          window_taps<L, 1, true>(V4, q, ng, fb, aw, av);
+        } else if (dm == 2) {
+          window_taps<L, 2, true>(V4, q, ng, fb, aw, av);
+        } else {
+          aw = make_float4(0.f, 0.f, 0.f, 0.f);
+          av = aw;
+          const int dq = dm >> 2;
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            int qs = q - (dq * l) % ng;
+            if (qs < 0) qs += ng;
+            const float4 s = V4[qs];
+            fma4(aw, fb.h[l], s);
+            fma4(av, fb.g[l], s);
+          }
+        }
+        wrow[q] = aw;
+        vreg[k] = av;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kVecGroups; ++k) {
+      const int q = tid + k * T;
+      if (q < ng) V4[q] = vreg[k];
+    }
+    __syncthreads();
+  }
+  float4* vrow = reinterpret_cast<float4*>(wout + static_cast<long long>(level) * n);
+  for (int q = tid; q < ng; q += T) vrow[q] = V4[q];
+}
+
+// Synthesis: V in LDS, W_j staged through LDS; the next row W_{j-1} is prefetched into
+// registers while level j computes, so no global-load latency sits between barriers.
+constexpr int kSynGroups = 4;  // float4 groups per thread, 1024 threads -> n <= 16384
+
+template <int L>
+__global__ void __launch_bounds__(1024) imodwt_vec_kernel(const float* __restrict__ w, int n, int level,
+                                                          FilterBank fb, unsigned long long keep,
+                                                          float* __restrict__ x, long long ld_out) {
+  extern __shared__ __attribute__((aligned(16))) float4 sm4[];
+  const int ng = n >> 2;
+  float4* V4 = sm4;
+  float4* W4 = sm4 + ng;
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const long long b = blockIdx.x;
+  const float* win = w + b * static_cast<long long>(level + 1) * n;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool keepV = (keep >> level) & 1ull;
+  {
+    const float4* vr = reinterpret_cast<const float4*>(win + static_cast<long long>(level) * n);
+    for (int q = tid; q < ng; q += T) V4[q] = keepV ? vr[q] : z4;
+  }
+  float4 pre[kSynGroups];
+  auto load_row = [&](int j) {  // W_j (1-based) -> registers
+    const bool use = (keep >> (j - 1)) & 1ull;
+    const float4* wr = reinterpret_cast<const float4*>(win + static_cast<long long>(j - 1) * n);
+#pragma unroll
+    for (int k = 0; k < kSynGroups; ++k) {
+      const int q = tid + k * T;
+      pre[k] = (use && q < ng) ? wr[q] : z4;
+    }
+  };
+  load_row(level);
+#pragma unroll
+  for (int k = 0; k < kSynGroups; ++k) {
+    const int q = tid + k * T;
+    if (q < ng) W4[q] = pre[k];
+  }
+  __syncthreads();
+  for (int j = level; j >= 1; --j) {
+    if (j > 1) load_row(j - 1);  // prefetch; consumed after the next barrier
+    const bool useW = (keep >> (j - 1)) & 1ull;
+    const int dm = static_cast<int>((1ll << (j - 1)) % n);
+    float4 vreg[kSynGroups];
+#pragma unroll
+    for (int k = 0; k < kSynGroups; ++k) {
+      const int q = tid + k * T;
+      if (q < ng) {
+        float4 acc;
+        if (dm == 1 || dm == 2) {
+          float4 av, aw, bw, dummy;
+          if (dm == 1) {
+            window_taps<L, 1, false>(V4, q, ng, fb, dummy, av);
+            window_taps<L, 1, false>(W4, q, ng, fb, aw, bw);
+          } else {
+            window_taps<L, 2, false>(V4, q, ng, fb, dummy, av);
+            window_taps<L, 2, false>(W4, q, ng, fb, aw, bw);
+          }
+          acc = useW ? make_float4(av.x + aw.x, av.y + aw.y, av.z + aw.z, av.w + aw.w) : av;
+        } else {
+          acc = z4;
+          const int dq = dm >> 2;
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            int qs = q + (dq * l) % ng;
+            if (qs >= ng) qs -= ng;
+            fma4(acc, fb.g[l], V4[qs]);
+            if (useW) fma4(acc, fb.h[l], W4[qs]);
+          }
+        }
+        vreg[k] = acc;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSynGroups; ++k) {
+      const int q = tid + k * T;
+      if (q < ng) {
+        V4[q] = vreg[k];
+        if (j > 1) W4[q] = pre[k];
+      }
+    }
+    __syncthreads();
+  }
+  float4* xo = reinterpret_cast<float4*>(x + b * ld_out);
+  for (int q = tid; q < ng; q += T) xo[q] = V4[q];
+}
+
 static int modwt_block(int n) {
   int t = (n + kModwtMaxPerThread - 1) / kModwtMaxPerThread;
   t = ((t + 63) / 64) * 64;
@@ -252,7 +436,14 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
   const size_t lds = static_cast<size_t>((ni + 3) & ~3) * sizeof(float);
   const int block = modwt_block(ni);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (n_taps == 8) {
+  if (n_taps == 8 && ni >= 64 && (ni & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 4 * kVecGroups * 512) {
+    int t = (ni / 4 + kVecGroups - 1) / kVecGroups;
+    t = ((t + 63) / 64) * 64;
+    t = t < 64 ? 64 : (t > 512 ? 512 : t);
+    allow_lds(modwt_vec_kernel<8>, lds);
+    hipLaunchKernelGGL(modwt_vec_kernel<8>, dim3(batch), dim3(t), lds, st, x, ld, ni, level, fb, w);
+  } else if (n_taps == 8) {
     allow_lds(modwt_kernel<8>, lds);
     hipLaunchKernelGGL(modwt_kernel<8>, dim3(batch), dim3(block), lds, st, x, ld, ni, level, n_taps, fb, w);
   } else {
@@ -274,7 +465,15 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
   const size_t lds = 2 * static_cast<size_t>((ni + 3) & ~3) * sizeof(float);
   const int block = modwt_block(ni);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (n_taps == 8) {
+  if (n_taps == 8 && ni >= 64 && (ni & 3) == 0 && (ld_out & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 4 * kSynGroups * 1024) {
+    int t = (ni / 4 + kSynGroups - 1) / kSynGroups;
+    t = ((t + 63) / 64) * 64;
+    t = t < 64 ? 64 : (t > 1024 ? 1024 : t);
+    allow_lds(imodwt_vec_kernel<8>, lds);
+    hipLaunchKernelGGL(imodwt_vec_kernel<8>, dim3(batch), dim3(t), lds, st, w, ni, level, fb, keep_mask, x,
+                       ld_out);
+  } else if (n_taps == 8) {
     allow_lds(imodwt_kernel<8>, lds);
     hipLaunchKernelGGL(imodwt_kernel<8>, dim3(batch), dim3(block), lds, st, w, ni, level, n_taps, fb,
                        keep_mask, x, ld_out);

@@ -32,7 +32,7 @@ constexpr int kWctMaxChunk = 512;
 
 // bins this thread owns: kk = t + (m < 8 ? m : m - 16) * NT
 template <int LOGN>
-__device__ __forceinline__ void smooth_filter(float2 (&v)[16], float beta, float scale, int t) {
+__device__ __forceinline__ void smooth_filter(cpx (&v)[16], float beta, float scale, int t) {
   using P = FftPlan<LOGN>;
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
@@ -44,10 +44,10 @@ __device__ __forceinline__ void smooth_filter(float2 (&v)[16], float beta, float
 
 // Forward spectra of both series of every pair: spec[b][which][k], natural order.
 template <int LOGN>
-__global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, float2* __restrict__ spec) {
+__global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, cpx* __restrict__ spec) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  __shared__ float2 lds[G::ROWS * P::PADN];
+  __shared__ cpx lds[G::ROWS * P::PADN];
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = tid - g * P::NT;
@@ -56,17 +56,17 @@ __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, f
   const bool valid = item < 2 * a.batch;
   const long long b = valid ? item >> 1 : 0;
   const int which = static_cast<int>(item & 1);
-  float2 tw[P::NTW_ALLOC];
+  cpx tw[P::NTW_ALLOC];
   fft_twiddles<LOGN>(tw, t);
   int par = 0;
-  float2 X[16];
+  cpx X[16];
   if (which == 0)
     load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
   else
     load_series<LOGN>(X, a.x2, a.affine2, b, a.ld, a.n0, t);
   fft_row<LOGN, -1, 1>(X, lds + g * P::PADN, 0, tw, t, par);
   if (!valid) return;
-  float2* o = spec + (2 * b + which) * static_cast<long long>(P::N);
+  cpx* o = spec + (2 * b + which) * static_cast<long long>(P::N);
 #pragma unroll
   for (int m = 0; m < 16; ++m) o[t + m * P::NT] = X[m];
 }
@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, f
 // The spectra are loop-invariant: an opaque pointer stops the compiler from hoisting
 // the 2 x 16 loads out of the scale loop (which costs 64 VGPRs and spills).
 template <int LOGN>
-__device__ __forceinline__ void load_spec(float2 (&X)[16], const float2* row, int t) {
+__device__ __forceinline__ void load_spec(cpx (&X)[16], const cpx* row, int t) {
   using P = FftPlan<LOGN>;
   asm volatile("" : "+s"(row));
 #pragma unroll
@@ -83,12 +83,12 @@ __device__ __forceinline__ void load_spec(float2 (&X)[16], const float2* row, in
 
 template <int LOGN>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
-    wct_phase_a(CwtArgs a, const float2* __restrict__ spec, float4* __restrict__ T) {
+    wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  __shared__ float2 lds[G::ROWS * P::PADN + 2 * kWctMaxChunk];
-  float2* prm_tab = lds + G::ROWS * P::PADN;      // (alpha, log2 c) of the Morlet filter
-  float2* smt_tab = prm_tab + kWctMaxChunk;       // (beta, 1/(N s)) of the time smoother
+  __shared__ cpx lds[G::ROWS * P::PADN + 2 * kWctMaxChunk];
+  cpx* prm_tab = lds + G::ROWS * P::PADN;      // (alpha, log2 c) of the Morlet filter
+  cpx* smt_tab = prm_tab + kWctMaxChunk;       // (beta, 1/(N s)) of the time smoother
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = tid - g * P::NT;
@@ -97,19 +97,19 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   const int ch = static_cast<int>(blk - b * a.nchunks);
   const int j0 = ch * a.chunk;
   const int j1 = min(a.S, j0 + a.chunk);
-  float2* my = lds + g * P::PADN;
+  cpx* my = lds + g * P::PADN;
   constexpr int bufstride = 0;
-  const float2* spec1 = spec + 2 * b * static_cast<long long>(P::N);
-  const float2* spec2 = spec1 + P::N;
+  const cpx* spec1 = spec + 2 * b * static_cast<long long>(P::N);
+  const cpx* spec2 = spec1 + P::N;
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const double s = a.scales[j0 + i];
     prm_tab[i] = morlet_params(s, a.dt, P::N);
     const double sn = s / a.dt * 2.0 * kPi / P::N;  // (s/dt) * (2 pi / N)
-    smt_tab[i] = make_float2(static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn),
+    smt_tab[i] = mkc(static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn),
                              static_cast<float>(1.0 / (static_cast<double>(P::N) * s)));
   }
-  float2 tw[P::NTW_ALLOC];
+  cpx tw[P::NTW_ALLOC];
   fft_twiddles<LOGN>(tw, t);
   int par = 0;
   __syncthreads();
@@ -119,9 +119,9 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   for (int it = 0; it < iters; ++it) {
     const int jl = it * G::ROWS + g;
     const bool valid = jl < j1 - j0;
-    const float2 prm = prm_tab[valid ? jl : 0];
-    const float2 smt = smt_tab[valid ? jl : 0];
-    float2 w1[16], v[16];
+    const cpx prm = prm_tab[valid ? jl : 0];
+    const cpx smt = smt_tab[valid ? jl : 0];
+    cpx w1[16], v[16];
     load_spec<LOGN>(w1, spec1, t);
     morlet_filter<LOGN>(v, w1, prm, f0, t);
     fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
@@ -132,37 +132,51 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
     const int j = j0 + jl;
     const long long rowbase = (b * a.S + (valid ? j : j0)) * static_cast<long long>(a.n0);
-    float* urow = a.out_u ? a.out_u + rowbase : nullptr;
-    float* vrow = a.out_v ? a.out_v + rowbase : nullptr;
-    const bool arrows = valid && urow != nullptr;
-    // W12 -> arrows; build z1 = |W1|^2 + i |W2|^2 and z2 = W12 (zero past n0: the
-    // reference smooths the row zero-padded to N)
+    float* urow = valid && a.out_u ? a.out_u + rowbase : nullptr;
+    float* vrow = valid && a.out_v ? a.out_v + rowbase : nullptr;
+    float* prow = valid && a.out_pow ? a.out_pow + rowbase : nullptr;
+    float* arow = valid && a.out_sig ? a.out_sig + rowbase : nullptr;  // phase angle
+    // W12 -> |W12|^2, angle, arrows; then z1 = |W1|^2 + i |W2|^2 and z2 = W12 (zero
+    // past n0: the reference smooths the row zero-padded to N)
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int pos = t + m * P::NT;
-      const float2 w12 = cmul(w1[m], cconj(v[m]));
+      const cpx w12 = cmul(w1[m], cconj(v[m]));
       const bool in = pos < a.n0;
-      if (arrows && in) {
-        const float r = sqrtf(cabs2(w12));
-        urow[pos] = r > 0.f ? w12.y / r : 0.f;
-        vrow[pos] = r > 0.f ? w12.x / r : 1.f;
+      if (in) {
+        const float p2 = cabs2(w12);
+        if (prow) prow[pos] = p2;
+        if (arow) arow[pos] = atan2f(w12.y, w12.x);
+        if (urow) {
+          const float r = sqrtf(p2);
+          urow[pos] = r > 0.f ? w12.y / r : 0.f;
+          vrow[pos] = r > 0.f ? w12.x / r : 1.f;
+        }
       }
-      const float2 z1 = make_float2(cabs2(w1[m]), cabs2(v[m]));
-      w1[m] = in ? w12 : make_float2(0.f, 0.f);
-      v[m] = in ? z1 : make_float2(0.f, 0.f);
+      const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
+      w1[m] = in ? w12 : mkc(0.f, 0.f);
+      v[m] = in ? z1 : mkc(0.f, 0.f);
     }
     fft_row<LOGN, -1, 1>(v, my, bufstride, tw, t, par);
     smooth_filter<LOGN>(v, smt.x, smt.y, t);
     fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
+    if (valid) {
+      cpx* ta = TA + rowbase;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int pos = t + m * P::NT;
+        if (pos < a.n0) ta[pos] = v[m];  // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
+      }
+    }
     fft_row<LOGN, -1, 1>(w1, my, bufstride, tw, t, par);
     smooth_filter<LOGN>(w1, smt.x, smt.y, t);
     fft_row<LOGN, 1, 1>(w1, my, bufstride, tw, t, par);
     if (!valid) continue;
-    float4* trow = T + rowbase;
+    cpx* tb = TB + rowbase;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int pos = t + m * P::NT;
-      if (pos < a.n0) trow[pos] = make_float4(v[m].x, v[m].y, w1[m].x, w1[m].y);
+      if (pos < a.n0) tb[pos] = w1[m];  // smoothed W12/s
     }
   }
 }
@@ -171,8 +185,8 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
 // end weights 0.5; the normalisation 1/(K-1) cancels in |S12|^2 / (S1 S2) but is kept
 // so the smoothed fields match the reference.
 template <int K>
-__global__ void __launch_bounds__(256) wct_phase_b(const float4* __restrict__ T, long long batch, int n0,
-                                                   int S, float* __restrict__ coh) {
+__global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, const cpx* __restrict__ TB,
+                                                   long long batch, int n0, int S, float* __restrict__ coh) {
   const long long tiles = (n0 + 255) / 256;
   const long long b = blockIdx.x / tiles;
   const int tcol = static_cast<int>((blockIdx.x - b * tiles) * 256 + threadIdx.x);
@@ -180,7 +194,8 @@ __global__ void __launch_bounds__(256) wct_phase_b(const float4* __restrict__ T,
   constexpr int LO = K / 2;        // rows before i
   constexpr int HI = (K - 1) / 2;  // rows after i
   const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
-  const float4* col = T + b * static_cast<long long>(S) * n0 + tcol;
+  const cpx* cola = TA + b * static_cast<long long>(S) * n0 + tcol;
+  const cpx* colb = TB + b * static_cast<long long>(S) * n0 + tcol;
   float* out = coh + b * static_cast<long long>(S) * n0 + tcol;
   float4 ring[K];
 #pragma unroll
@@ -190,7 +205,12 @@ __global__ void __launch_bounds__(256) wct_phase_b(const float4* __restrict__ T,
 #pragma unroll
     for (int r = 0; r < K; ++r) {
       const int j = jb + r;
-      ring[r] = j < S ? col[static_cast<long long>(j) * n0] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (j < S) {
+        const cpx ta = cola[static_cast<long long>(j) * n0], tb = colb[static_cast<long long>(j) * n0];
+        ring[r] = make_float4(ta.x, ta.y, tb.x, tb.y);
+      } else {
+        ring[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
       const int i = j - HI;
       if (i >= 0 && i < S) {
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -214,7 +234,7 @@ __global__ void __launch_bounds__(256) wct_phase_b(const float4* __restrict__ T,
 }
 
 template <int LOGN>
-static int launch_phase_a(CwtArgs& a, float2* spec, float4* T, hipStream_t st) {
+static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, hipStream_t st) {
   using G = WctGeom<LOGN>;
   {
     const long long items = 2 * a.batch;
@@ -238,16 +258,17 @@ static int launch_phase_a(CwtArgs& a, float2* spec, float4* T, hipStream_t st) {
   a.chunk = chunk;
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  hipLaunchKernelGGL(wct_phase_a<LOGN>, dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, T);
+  hipLaunchKernelGGL(wct_phase_a<LOGN>, dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, TA, TB);
   return launch_status();
 }
 
 template <int K>
-static int launch_phase_b(const float4* T, long long batch, int n0, int S, float* coh, hipStream_t st) {
+static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0, int S, float* coh,
+                          hipStream_t st) {
   const long long tiles = (n0 + 255) / 256;
   const long long grid = batch * tiles;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  hipLaunchKernelGGL(wct_phase_b<K>, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, T, batch, n0,
+  hipLaunchKernelGGL(wct_phase_b<K>, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB, batch, n0,
                      S, coh);
   return launch_status();
 }
@@ -262,23 +283,23 @@ static int log2_ceil_w(long long n) {
 
 using namespace wtmi;
 
-// workspace = [T: batch x S x n0 float4][spectra: batch x 2 x N float2]
+// workspace = [T: batch x S x n0 float4][spectra: batch x 2 x N cpx]
 static long long wct_t_bytes(long long batch, long long n0, int n_scales) {
-  const long long b = batch * n0 * static_cast<long long>(n_scales) * static_cast<long long>(sizeof(float4));
-  return (b + 255) & ~255ll;
+  const long long b = batch * n0 * static_cast<long long>(n_scales) * static_cast<long long>(sizeof(cpx));
+  return 2 * ((b + 255) & ~255ll);
 }
 
 extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales) {
   if (batch < 0 || n0 < 0 || n_scales < 0) return -1;
   const long long N = 1ll << log2_ceil_w(n0 < 1 ? 1 : n0);
-  return wct_t_bytes(batch, n0, n_scales) + batch * 2 * N * static_cast<long long>(sizeof(float2));
+  return wct_t_bytes(batch, n0, n_scales) + batch * 2 * N * static_cast<long long>(sizeof(cpx));
 }
 
 extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
                                long long n0, const double* affine1, const double* affine2,
                                const double* scales, int n_scales, double dt, double f0, int boxcar,
-                               void* workspace, float* out_coh, float* out_u, float* out_v,
-                               void* stream) {
+                               void* workspace, float* out_coh, float* out_power, float* out_phase,
+                               float* out_u, float* out_v, void* stream) {
   if (!x1 || !x2 || !scales || !workspace || !out_coh || n0 < 0 || batch < 0 || n_scales < 0 ||
       ld < n0 || boxcar < 1)
     return kErrArg;
@@ -301,12 +322,16 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   a.f0 = f0;
   a.out_u = out_u;
   a.out_v = out_v;
+  a.out_pow = out_power;
+  a.out_sig = out_phase;  // phase-angle plane (atan2 of W12)
   hipStream_t st = static_cast<hipStream_t>(stream);
-  float4* T = static_cast<float4*>(workspace);
-  float2* spec = reinterpret_cast<float2*>(static_cast<char*>(workspace) + wct_t_bytes(batch, n0, n_scales));
+  const long long plane = wct_t_bytes(batch, n0, n_scales) / 2;
+  cpx* TA = static_cast<cpx*>(workspace);
+  cpx* TB = reinterpret_cast<cpx*>(static_cast<char*>(workspace) + plane);
+  cpx* spec = reinterpret_cast<cpx*>(static_cast<char*>(workspace) + 2 * plane);
   int rc;
   switch (logn) {
-#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, T, st); break;
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, st); break;
     WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
     WTMI_A(12) WTMI_A(13) WTMI_A(14)
 #undef WTMI_A
@@ -315,7 +340,7 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   if (rc != kOk) return rc;
   const int n0i = static_cast<int>(n0);
   switch (boxcar) {
-#define WTMI_B(K) case K: return launch_phase_b<K>(T, batch, n0i, n_scales, out_coh, st);
+#define WTMI_B(K) case K: return launch_phase_b<K>(TA, TB, batch, n0i, n_scales, out_coh, st);
     WTMI_B(1) WTMI_B(2) WTMI_B(3) WTMI_B(4) WTMI_B(5) WTMI_B(6) WTMI_B(7) WTMI_B(8)
     WTMI_B(9) WTMI_B(10) WTMI_B(11) WTMI_B(12) WTMI_B(13) WTMI_B(14) WTMI_B(15) WTMI_B(16)
     WTMI_B(17) WTMI_B(18) WTMI_B(19) WTMI_B(20) WTMI_B(21) WTMI_B(22) WTMI_B(23) WTMI_B(24)

@@ -171,8 +171,10 @@ def wct_workspace_bytes(batch: int, n0: int, n_scales: int) -> int:
 
 def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
                boxcar: int, affine1=None, affine2=None, want_uv: bool = True,
+               want_power: bool = False, want_phase: bool = False,
                workspace: Optional[torch.Tensor] = None):
-    """Wavelet coherence of row pairs; returns dict coh [B,S,n0] (+ u, v)."""
+    """Wavelet coherence of row pairs; returns dict coh [B,S,n0] (+ u, v, power =
+    |W1 W2*|^2, phase = angle(W1 W2*))."""
     x1 = _rows(x1).to(torch.float32)
     x2 = _rows(x2).to(torch.float32)
     if x1.shape != x2.shape:
@@ -188,6 +190,10 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     shape = (B, S, n0)
     res = {"coh": torch.empty(shape, dtype=torch.float32, device=dev)}
+    if want_power:
+        res["power"] = torch.empty(shape, dtype=torch.float32, device=dev)
+    if want_phase:
+        res["phase"] = torch.empty(shape, dtype=torch.float32, device=dev)
     if want_uv:
         res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
         res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
@@ -196,7 +202,8 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     with torch.cuda.device(dev):
         _lib.call("wtmi_wct_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
                   _ptr(sc), S, float(dt), float(f0), int(boxcar), _ptr(workspace),
-                  _ptr(res["coh"]), _ptr(res.get("u")), _ptr(res.get("v")), _stream(dev))
+                  _ptr(res["coh"]), _ptr(res.get("power")), _ptr(res.get("phase")),
+                  _ptr(res.get("u")), _ptr(res.get("v")), _stream(dev))
     return res
 
 
@@ -277,3 +284,62 @@ def waverec(coeffs: torch.Tensor, n: int, rec_lo, rec_hi, level: int,
                   hi.ctypes.data_as(VP), lo.size, int(level), _ptr(masks), len(keep_masks),
                   _ptr(out), out_len, _stream(dev))
     return out
+
+
+# ------------------------------------------------------------ torch custom ops
+# torch.ops.wtmi.* wrappers over the same HIP kernels (CUDA/ROCm dispatch only: a
+# CPU tensor has no kernel and raises).  Filter taps travel as host float64 tensors.
+def _register():
+    lib = torch.library
+
+    @lib.custom_op("wtmi::cwt", mutates_args=())
+    def _cwt(x: torch.Tensor, scales: torch.Tensor, dt: float, f0: float) -> torch.Tensor:
+        return cwt_morlet(x, scales, dt, f0)["w"]
+
+    @_cwt.register_fake
+    def _(x, scales, dt, f0):
+        return x.new_empty((x.shape[0] if x.dim() == 2 else 1, scales.numel(), x.shape[-1]),
+                           dtype=torch.complex64)
+
+    @lib.custom_op("wtmi::cwt_power", mutates_args=())
+    def _cwt_power(x: torch.Tensor, scales: torch.Tensor, dt: float, f0: float) -> torch.Tensor:
+        return cwt_morlet(x, scales, dt, f0, want_w=False, want_power=True)["power"]
+
+    @_cwt_power.register_fake
+    def _(x, scales, dt, f0):
+        return x.new_empty((x.shape[0] if x.dim() == 2 else 1, scales.numel(), x.shape[-1]),
+                           dtype=torch.float32)
+
+    @lib.custom_op("wtmi::wct", mutates_args=())
+    def _wct(x1: torch.Tensor, x2: torch.Tensor, scales: torch.Tensor, dt: float, f0: float,
+             boxcar: int) -> torch.Tensor:
+        return wct_morlet(x1, x2, scales, dt, f0, boxcar=boxcar, want_uv=False)["coh"]
+
+    @_wct.register_fake
+    def _(x1, x2, scales, dt, f0, boxcar):
+        return x1.new_empty((x1.shape[0] if x1.dim() == 2 else 1, scales.numel(), x1.shape[-1]),
+                            dtype=torch.float32)
+
+    @lib.custom_op("wtmi::modwt", mutates_args=())
+    def _modwt(x: torch.Tensor, dec_lo: torch.Tensor, dec_hi: torch.Tensor, level: int
+               ) -> torch.Tensor:
+        return modwt(x, dec_lo.cpu().numpy(), dec_hi.cpu().numpy(), level)
+
+    @_modwt.register_fake
+    def _(x, dec_lo, dec_hi, level):
+        return x.new_empty((x.shape[0] if x.dim() == 2 else 1, level + 1, x.shape[-1]),
+                           dtype=torch.float32)
+
+    @lib.custom_op("wtmi::imodwt", mutates_args=())
+    def _imodwt(w: torch.Tensor, dec_lo: torch.Tensor, dec_hi: torch.Tensor) -> torch.Tensor:
+        return imodwt(w, dec_lo.cpu().numpy(), dec_hi.cpu().numpy())
+
+    @_imodwt.register_fake
+    def _(w, dec_lo, dec_hi):
+        return w.new_empty((w.shape[0] if w.dim() == 3 else 1, w.shape[-1]), dtype=torch.float32)
+
+
+try:
+    torch.ops.wtmi.cwt  # already registered (module reloaded)
+except (AttributeError, RuntimeError):
+    _register()

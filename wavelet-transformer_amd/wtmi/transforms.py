@@ -241,7 +241,7 @@ def boxcar_rows(wavelet: Morlet, dj: float) -> int:
 
 
 def wct_batch(y1: torch.Tensor, y2: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wavelet="morlet",
-              normalize=True, want_uv=True, workspace=None):
+              normalize=True, want_uv=True, want_power=False, want_phase=False, workspace=None):
     """Batched coherence of device row pairs: (dict coh/u/v, sj, freqs)."""
     wavelet = as_morlet(wavelet)
     if wavelet.deltaj0 <= 0:
@@ -253,7 +253,8 @@ def wct_batch(y1: torch.Tensor, y2: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wa
         a1 = normalize_coefs(ops.series_moments(y1))
         a2 = normalize_coefs(ops.series_moments(y2))
     res = ops.wct_morlet(y1, y2, sj, dt, wavelet.f0, boxcar=boxcar_rows(wavelet, dj), affine1=a1,
-                         affine2=a2, want_uv=want_uv, workspace=workspace)
+                         affine2=a2, want_uv=want_uv, want_power=want_power,
+                         want_phase=want_phase, workspace=workspace)
     return res, sj, freqs
 
 
@@ -271,11 +272,10 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
     d1, d2 = _to_dev(y1).reshape(1, -1), _to_dev(y2).reshape(1, -1)
     x1 = _norm32(d1) if normalize else d1.to(torch.float32)
     x2 = _norm32(d2) if normalize else d2.to(torch.float32)
-    res, sj, freq = wct_batch(x1, x2, dt, dj, s0, J, wavelet, normalize=False, want_uv=True)
-    u, v = res["u"][0], res["v"][0]
-    aWCT = torch.atan2(u, v)
+    res, sj, freq = wct_batch(x1, x2, dt, dj, s0, J, wavelet, normalize=False, want_uv=False,
+                              want_phase=True)
     n0 = d1.shape[1]
-    return (_np(res["coh"][0], np.float64), _np(aWCT, np.float64),
+    return (_np(res["coh"][0], np.float64), _np(res["phase"][0], np.float64),
             cone_of_influence(n0, dt, wavelet), freq, np.asarray([0]))
 
 
