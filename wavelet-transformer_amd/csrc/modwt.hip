@@ -218,7 +218,6 @@ __global__ void __launch_bounds__(1024) imodwt_kernel(const float* __restrict__ 
 // 4 consecutive samples (float4).  Levels j >= 3 have a dilation that is a multiple
 // of 4, so every tap is one aligned ds_read_b128; levels 1 and 2 read a register
 // window of 3 / 5 aligned float4 blocks and form all taps from it.
-constexpr int kVecGroups = 8;  // float4 groups per thread (n <= 4 * 8 * block)
 
 template <int L, int DM, bool FWD>
 __device__ __forceinline__ void window_taps(const float4* __restrict__ V4, int q, int ng,
@@ -249,17 +248,27 @@ __device__ __forceinline__ void window_taps(const float4* __restrict__ V4, int q
   b = make_float4(rb[0], rb[1], rb[2], rb[3]);
 }
 
+// Materialise a value here: stops the compiler from sinking the math that produced it
+// past a barrier into its (conditional) consumer, which keeps every LDS operand live.
+__device__ __forceinline__ void pin4(float4& v) {
+  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
 __device__ __forceinline__ void fma4(float4& acc, float c, const float4& s) {
   acc.x = fmaf(c, s.x, acc.x); acc.y = fmaf(c, s.y, acc.y);
   acc.z = fmaf(c, s.z, acc.z); acc.w = fmaf(c, s.w, acc.w);
 }
 
-template <int L>
-__global__ void __launch_bounds__(512, 2) modwt_vec_kernel(const float* __restrict__ x, long long ld,
-                                                           int n, int level, FilterBank fb,
-                                                           float* __restrict__ w) {
+// Analysis: V_{j-1} in LDS (n floats), each thread owns GROUPS float4 groups (stride T).
+// The level loop re-derives its addresses from an opaque copy of tid and pins each
+// result before the barrier; without both, the compiler hoists per-group address math
+// out of the level loop and sinks the tap FMAs past the barrier, keeping every LDS
+// operand live (256 VGPRs + spills).
+template <int L, int GROUPS, int T>
+__global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ x, long long ld,
+                                                      int n, int level, FilterBank fb,
+                                                      float* __restrict__ w) {
   extern __shared__ __attribute__((aligned(16))) float4 V4[];
-  const int T = blockDim.x;
   const int tid = threadIdx.x;
   const long long b = blockIdx.x;
   const int ng = n >> 2;
@@ -270,37 +279,38 @@ __global__ void __launch_bounds__(512, 2) modwt_vec_kernel(const float* __restri
   for (int j = 1; j <= level; ++j) {
     const int dm = static_cast<int>((1ll << (j - 1)) % n);
     float4* wrow = reinterpret_cast<float4*>(wout + static_cast<long long>(j - 1) * n);
-    float4 vreg[kVecGroups];
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
+    float4 vreg[GROUPS];
 #pragma unroll
-    for (int k = 0; k < kVecGroups; ++k) {
-      const int q = tid + k * T;
-      if (q < ng) {
-        float4 aw, av;
-        if (dm == 1) {
-          window_taps<L, 1, true>(V4, q, ng, fb, aw, av);
-        } else if (dm == 2) {
-          window_taps<L, 2, true>(V4, q, ng, fb, aw, av);
-        } else {
-          aw = make_float4(0.f, 0.f, 0.f, 0.f);
-          av = aw;
-          const int dq = dm >> 2;
+    for (int k = 0; k < GROUPS; ++k) {
+      const int q = min(tl + k * T, ng - 1);
+      float4 aw, av;
+      if (dm == 1) {
+        window_taps<L, 1, true>(V4, q, ng, fb, aw, av);
+      } else if (dm == 2) {
+        window_taps<L, 2, true>(V4, q, ng, fb, aw, av);
+      } else {
+        aw = make_float4(0.f, 0.f, 0.f, 0.f);
+        av = aw;
+        const int dq = dm >> 2;
 #pragma unroll
-          for (int l = 0; l < L; ++l) {
-            int qs = q - (dq * l) % ng;
-            if (qs < 0) qs += ng;
-            const float4 s = V4[qs];
-            fma4(aw, fb.h[l], s);
-            fma4(av, fb.g[l], s);
-          }
+        for (int l = 0; l < L; ++l) {
+          int qs = q - (dq * l) % ng;
+          if (qs < 0) qs += ng;
+          const float4 s = V4[qs];
+          fma4(aw, fb.h[l], s);
+          fma4(av, fb.g[l], s);
         }
-        wrow[q] = aw;
-        vreg[k] = av;
       }
+      if (tl + k * T < ng) wrow[q] = aw;
+      vreg[k] = av;
+      pin4(vreg[k]);
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kVecGroups; ++k) {
-      const int q = tid + k * T;
+    for (int k = 0; k < GROUPS; ++k) {
+      const int q = tl + k * T;
       if (q < ng) V4[q] = vreg[k];
     }
     __syncthreads();
@@ -309,19 +319,65 @@ __global__ void __launch_bounds__(512, 2) modwt_vec_kernel(const float* __restri
   for (int q = tid; q < ng; q += T) vrow[q] = V4[q];
 }
 
-// Synthesis: V in LDS, W_j staged through LDS; the next row W_{j-1} is prefetched into
-// registers while level j computes, so no global-load latency sits between barriers.
-constexpr int kSynGroups = 4;  // float4 groups per thread, 1024 threads -> n <= 16384
+// Synthesis: V and W_j in LDS (128 KiB: one workgroup per CU).  GROUPS float4 groups
+// per thread (GROUPS * 4 * threads >= n).  PREFETCH: the next row W_{j-1} is loaded
+// into registers while level j computes (costs 4*GROUPS VGPRs); otherwise each level
+// starts with a direct global -> LDS copy of W_j.
+template <int L, int GROUPS, int T>
+__device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const float4* __restrict__ W4,
+                                          int ng, int dm, float wsel, const FilterBank& fb, int tid,
+                                          float4 (&vreg)[GROUPS]) {
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (dm == 1 || dm == 2) {
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) {
+      int q = min(tid + k * T, ng - 1);
+      asm volatile("" : "+v"(q));  // keep tap addresses out of LICM (VGPR blow-up)
+      float4 av, aw, bw, dummy;
+      if (dm == 1) {
+        window_taps<L, 1, false>(V4, q, ng, fb, dummy, av);
+        window_taps<L, 1, false>(W4, q, ng, fb, aw, bw);
+      } else {
+        window_taps<L, 2, false>(V4, q, ng, fb, dummy, av);
+        window_taps<L, 2, false>(W4, q, ng, fb, aw, bw);
+      }
+      vreg[k] = make_float4(fmaf(wsel, aw.x, av.x), fmaf(wsel, aw.y, av.y), fmaf(wsel, aw.z, av.z),
+                            fmaf(wsel, aw.w, av.w));
+      pin4(vreg[k]);
+    }
+  } else {
+    const int dq = dm >> 2;
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) {
+      int q = min(tid + k * T, ng - 1);
+      asm volatile("" : "+v"(q));  // keep tap addresses out of LICM (VGPR blow-up)
+      float4 acc = z4;
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        int qs = q + (dq * l) % ng;
+        if (qs >= ng) qs -= ng;
+        fma4(acc, fb.g[l], V4[qs]);
+        fma4(acc, wsel * fb.h[l], W4[qs]);
+      }
+      vreg[k] = acc;
+      pin4(vreg[k]);
+    }
+  }
+}
 
-template <int L>
-__global__ void __launch_bounds__(1024) imodwt_vec_kernel(const float* __restrict__ w, int n, int level,
-                                                          FilterBank fb, unsigned long long keep,
-                                                          float* __restrict__ x, long long ld_out) {
+// MODE 0: W_j copied global -> LDS at the start of each level.
+// MODE 1: as 0, but W_{j-1} is prefetched into registers while level j computes.
+// MODE 2: W_j taps read straight from global memory (L1/L2); LDS holds V only (n floats),
+//         so two workgroups fit per CU and one's loads overlap the other's math.
+template <int L, int GROUPS, int T, int MODE>
+__global__ void __launch_bounds__(T)
+    imodwt_vec_kernel(const float* __restrict__ w, int n, int level, FilterBank fb, unsigned long long keep,
+                      float* __restrict__ x, long long ld_out) {
+  constexpr bool PREFETCH = MODE == 1;
   extern __shared__ __attribute__((aligned(16))) float4 sm4[];
   const int ng = n >> 2;
   float4* V4 = sm4;
   float4* W4 = sm4 + ng;
-  const int T = blockDim.x;
   const int tid = threadIdx.x;
   const long long b = blockIdx.x;
   const float* win = w + b * static_cast<long long>(level + 1) * n;
@@ -331,68 +387,42 @@ __global__ void __launch_bounds__(1024) imodwt_vec_kernel(const float* __restric
     const float4* vr = reinterpret_cast<const float4*>(win + static_cast<long long>(level) * n);
     for (int q = tid; q < ng; q += T) V4[q] = keepV ? vr[q] : z4;
   }
-  float4 pre[kSynGroups];
-  auto load_row = [&](int j) {  // W_j (1-based) -> registers
-    const bool use = (keep >> (j - 1)) & 1ull;
-    const float4* wr = reinterpret_cast<const float4*>(win + static_cast<long long>(j - 1) * n);
+  float4 pre[GROUPS];
+  if (PREFETCH) {
+    const float4* wr = reinterpret_cast<const float4*>(win + static_cast<long long>(level - 1) * n);
 #pragma unroll
-    for (int k = 0; k < kSynGroups; ++k) {
-      const int q = tid + k * T;
-      pre[k] = (use && q < ng) ? wr[q] : z4;
-    }
-  };
-  load_row(level);
+    for (int k = 0; k < GROUPS; ++k) pre[k] = wr[min(tid + k * T, ng - 1)];
 #pragma unroll
-  for (int k = 0; k < kSynGroups; ++k) {
-    const int q = tid + k * T;
-    if (q < ng) W4[q] = pre[k];
+    for (int k = 0; k < GROUPS; ++k)
+      if (tid + k * T < ng) W4[tid + k * T] = pre[k];
   }
-  __syncthreads();
   for (int j = level; j >= 1; --j) {
-    if (j > 1) load_row(j - 1);  // prefetch; consumed after the next barrier
-    const bool useW = (keep >> (j - 1)) & 1ull;
-    const int dm = static_cast<int>((1ll << (j - 1)) % n);
-    float4 vreg[kSynGroups];
+    const float4* wr = reinterpret_cast<const float4*>(win + static_cast<long long>(j - 1) * n);
+    if (MODE == 0)
+      for (int q = tid; q < ng; q += T) W4[q] = wr[q];
+    __syncthreads();
+    if (PREFETCH && j > 1) {
+      const float4* wn = reinterpret_cast<const float4*>(win + static_cast<long long>(j - 2) * n);
 #pragma unroll
-    for (int k = 0; k < kSynGroups; ++k) {
-      const int q = tid + k * T;
-      if (q < ng) {
-        float4 acc;
-        if (dm == 1 || dm == 2) {
-          float4 av, aw, bw, dummy;
-          if (dm == 1) {
-            window_taps<L, 1, false>(V4, q, ng, fb, dummy, av);
-            window_taps<L, 1, false>(W4, q, ng, fb, aw, bw);
-          } else {
-            window_taps<L, 2, false>(V4, q, ng, fb, dummy, av);
-            window_taps<L, 2, false>(W4, q, ng, fb, aw, bw);
-          }
-          acc = useW ? make_float4(av.x + aw.x, av.y + aw.y, av.z + aw.z, av.w + aw.w) : av;
-        } else {
-          acc = z4;
-          const int dq = dm >> 2;
-#pragma unroll
-          for (int l = 0; l < L; ++l) {
-            int qs = q + (dq * l) % ng;
-            if (qs >= ng) qs -= ng;
-            fma4(acc, fb.g[l], V4[qs]);
-            if (useW) fma4(acc, fb.h[l], W4[qs]);
-          }
-        }
-        vreg[k] = acc;
-      }
+      for (int k = 0; k < GROUPS; ++k) pre[k] = wn[min(tid + k * T, ng - 1)];
     }
+    const float wsel = ((keep >> (j - 1)) & 1ull) ? 1.f : 0.f;  // masked rows count as 0
+    const int dm = static_cast<int>((1ll << (j - 1)) % n);
+    int tl = tid;
+    asm volatile("" : "+v"(tl));  // per-level copy: keeps address math out of LICM
+    float4 vreg[GROUPS];
+    syn_level<L, GROUPS, T>(V4, MODE == 2 ? wr : W4, ng, dm, wsel, fb, tl, vreg);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kSynGroups; ++k) {
-      const int q = tid + k * T;
+    for (int k = 0; k < GROUPS; ++k) {
+      const int q = tl + k * T;
       if (q < ng) {
         V4[q] = vreg[k];
-        if (j > 1) W4[q] = pre[k];
+        if (PREFETCH && j > 1) W4[q] = pre[k];
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
   float4* xo = reinterpret_cast<float4*>(x + b * ld_out);
   for (int q = tid; q < ng; q += T) xo[q] = V4[q];
 }
@@ -437,12 +467,26 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
   const int block = modwt_block(ni);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n_taps == 8 && ni >= 64 && (ni & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 4 * kVecGroups * 512) {
-    int t = (ni / 4 + kVecGroups - 1) / kVecGroups;
-    t = ((t + 63) / 64) * 64;
-    t = t < 64 ? 64 : (t > 512 ? 512 : t);
-    allow_lds(modwt_vec_kernel<8>, lds);
-    hipLaunchKernelGGL(modwt_vec_kernel<8>, dim3(batch), dim3(t), lds, st, x, ld, ni, level, fb, w);
+      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 16384) {
+    const char* ev = getenv("WTMI_MODWT_VARIANT");
+    const int var = ev ? atoi(ev) : 0;
+    auto launch = [&](auto kernel, int t) {
+      allow_lds(kernel, lds);
+      hipLaunchKernelGGL(kernel, dim3(batch), dim3(t), lds, st, x, ld, ni, level, fb, w);
+    };
+    const int ng = ni / 4;
+    if (ng <= 256)
+      launch(modwt_vec_kernel<8, 1, 256>, 256);
+    else if (ng <= 512)
+      launch(modwt_vec_kernel<8, 1, 512>, 512);
+    else if (ng <= 1024)
+      launch(modwt_vec_kernel<8, 1, 1024>, 1024);
+    else if (ng <= 2048)
+      launch(modwt_vec_kernel<8, 2, 1024>, 1024);
+    else if (var == 1)
+      launch(modwt_vec_kernel<8, 4, 1024>, 1024);
+    else
+      launch(modwt_vec_kernel<8, 8, 512>, 512);  // C3 A/B: 1.62 vs 1.65 ms
   } else if (n_taps == 8) {
     allow_lds(modwt_kernel<8>, lds);
     hipLaunchKernelGGL(modwt_kernel<8>, dim3(batch), dim3(block), lds, st, x, ld, ni, level, n_taps, fb, w);
@@ -466,13 +510,34 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
   const int block = modwt_block(ni);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n_taps == 8 && ni >= 64 && (ni & 3) == 0 && (ld_out & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 4 * kSynGroups * 1024) {
-    int t = (ni / 4 + kSynGroups - 1) / kSynGroups;
-    t = ((t + 63) / 64) * 64;
-    t = t < 64 ? 64 : (t > 1024 ? 1024 : t);
-    allow_lds(imodwt_vec_kernel<8>, lds);
-    hipLaunchKernelGGL(imodwt_vec_kernel<8>, dim3(batch), dim3(t), lds, st, w, ni, level, fb, keep_mask, x,
-                       ld_out);
+      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 16384) {
+    const char* ev = getenv("WTMI_IMODWT_VARIANT");
+    const int var = ev ? atoi(ev) : 0;
+    auto launch = [&](auto kernel, int t) {
+      allow_lds(kernel, lds);
+      hipLaunchKernelGGL(kernel, dim3(batch), dim3(t), lds, st, w, ni, level, fb, keep_mask, x, ld_out);
+    };
+    auto launch_lds = [&](auto kernel, int t, size_t bytes) {
+      allow_lds(kernel, bytes);
+      hipLaunchKernelGGL(kernel, dim3(batch), dim3(t), bytes, st, w, ni, level, fb, keep_mask, x, ld_out);
+    };
+    const int ng = ni / 4;
+    if (ng <= 256)
+      launch(imodwt_vec_kernel<8, 1, 256, 0>, 256);
+    else if (ng <= 512)
+      launch(imodwt_vec_kernel<8, 1, 512, 0>, 512);
+    else if (ng <= 1024)
+      launch(imodwt_vec_kernel<8, 1, 1024, 0>, 1024);
+    else if (ng <= 2048)
+      launch(imodwt_vec_kernel<8, 2, 1024, 0>, 1024);
+    else if (var == 1)
+      launch(imodwt_vec_kernel<8, 4, 1024, 1>, 1024);
+    else if (var == 2)
+      launch_lds(imodwt_vec_kernel<8, 4, 1024, 2>, 1024, lds / 2);
+    else if (var == 3)
+      launch(imodwt_vec_kernel<8, 4, 1024, 0>, 1024);
+    else  // C3 A/B (ms): W from global, 2 WG/CU 2.00; W via LDS 2.11; + register prefetch 2.71
+      launch_lds(imodwt_vec_kernel<8, 8, 512, 2>, 512, lds / 2);
   } else if (n_taps == 8) {
     allow_lds(imodwt_kernel<8>, lds);
     hipLaunchKernelGGL(imodwt_kernel<8>, dim3(batch), dim3(block), lds, st, w, ni, level, n_taps, fb,

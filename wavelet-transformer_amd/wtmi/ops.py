@@ -212,20 +212,30 @@ def _taps(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
 
 
-def modwt(x: torch.Tensor, dec_lo, dec_hi, level: int) -> torch.Tensor:
+def _out(out, shape, dev):
+    if out is None:
+        return torch.empty(shape, dtype=torch.float32, device=dev)
+    if tuple(out.shape) != tuple(shape) or out.dtype != torch.float32 or not out.is_contiguous() \
+            or out.device != dev:
+        raise ValueError(f"out must be a contiguous float32 tensor of shape {tuple(shape)} on {dev}")
+    return out
+
+
+def modwt(x: torch.Tensor, dec_lo, dec_hi, level: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[B, n] float32 -> [B, level + 1, n] rows [W_1 .. W_J, V_J]."""
     x = _rows(x).to(torch.float32)
     dev = _check_dev(x)
     B, n = x.shape
     lo, hi = _taps(dec_lo), _taps(dec_hi)
-    w = torch.empty((B, level + 1, n), dtype=torch.float32, device=dev)
+    w = _out(out, (B, level + 1, n), dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_modwt", _ptr(x), x.stride(0), B, n, lo.ctypes.data_as(VP),
                   hi.ctypes.data_as(VP), lo.size, int(level), _ptr(w), _stream(dev))
     return w
 
 
-def imodwt(w: torch.Tensor, dec_lo, dec_hi, keep_mask: Optional[int] = None) -> torch.Tensor:
+def imodwt(w: torch.Tensor, dec_lo, dec_hi, keep_mask: Optional[int] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[B, J + 1, n] -> [B, n]; rows with a clear bit in keep_mask count as zero."""
     if w.dim() == 2:
         w = w.unsqueeze(0)
@@ -234,7 +244,7 @@ def imodwt(w: torch.Tensor, dec_lo, dec_hi, keep_mask: Optional[int] = None) -> 
     B, R, n = w.shape
     lo, hi = _taps(dec_lo), _taps(dec_hi)
     keep = (1 << 64) - 1 if keep_mask is None else int(keep_mask)
-    x = torch.empty((B, n), dtype=torch.float32, device=dev)
+    x = _out(out, (B, n), dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_imodwt", _ptr(w), B, n, lo.ctypes.data_as(VP), hi.ctypes.data_as(VP),
                   lo.size, R - 1, C.c_ulonglong(keep), _ptr(x), x.stride(0), _stream(dev))
