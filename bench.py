@@ -101,6 +101,7 @@ class C2:
         self.units = self.B * self.sj.size * self.n0
         self.bytes = self.units * 8 + self.B * self.n0 * 4  # W write + x read
         self.kernel = "cwt_morlet_kernel<12,1,0>"
+        self.per_step = {"wtmi::cwt_morlet_kernel<12": 1}
         self.unit_name = "coeffs/s"
         self.bytes_note = "8 B/coeff complex64 W write + 4 B/sample x read"
 
@@ -142,6 +143,7 @@ class C5(C2):
         self.units = self.B * self.sj.size * self.n0
         self.bytes = self.units * 8 + self.B * self.n0 * 4
         self.kernel = "cwt_morlet_kernel<13,1,0>"
+        self.per_step = {"wtmi::cwt_morlet_kernel<13": self.B // self.chunk}
         self.unit_name = "coeffs/s"
         self.bytes_note = "8 B/coeff complex64 W write + 4 B/sample x read"
 
@@ -178,7 +180,8 @@ class C3:
         self.x = torch.tensor(synth_batch(rng, self.B, self.n), device=dev)
         self.units = self.B * (self.J + 1) * self.n
         self.bytes = self.B * self.n * 96  # 4 x + 44 W write + 44 W read + 4 x^
-        self.kernel = "modwt_kernel<8>+imodwt_kernel<8>"
+        self.kernel = "modwt_vec_kernel<8,8,512>+imodwt_vec_kernel<8,8,512,2>"
+        self.per_step = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_vec_kernel<": 1}
         self.unit_name = "coeffs/s"
         self.bytes_note = "96 B per series-sample (x, W write, W read, x^)"
 
@@ -216,6 +219,7 @@ class C4:
         self.ws = torch.empty(ops.wct_workspace_bytes(self.P, self.n, S), dtype=torch.uint8,
                               device=dev)
         self.kernel = "wct_spectra<13>+wct_phase_a<13>+wct_phase_b<10>"
+        self.per_step = {"wtmi::wct_spectra<": 1, "wtmi::wct_phase_a<": 1, "wtmi::wct_phase_b<": 1}
         self.unit_name = "coeffs/s"
         self.bytes_note = "12 B/coeff (|W12|^2 + WCT + phase, f32) + 8 B/pair-sample inputs"
 
@@ -235,6 +239,28 @@ class C4:
 
 
 CONFIGS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5}
+
+
+def pmc_traffic(cfg, per_step):
+    """HBM bytes per step of the roofline kernels from the newest committed PMC pass
+    (profiles/rNN/pmc_traffic.json, written by scripts/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        with open(path) as fh:
+            ent = json.load(fh).get(cfg)
+        if not ent:
+            continue
+        total, seen = 0.0, 0
+        for prefix, count in per_step.items():
+            hits = [v for k, v in ent["kernels"].items() if k.startswith(prefix)]
+            if len(hits) != 1:
+                break
+            total += hits[0]["hbm_bytes"] * count
+            seen += 1
+        if seen == len(per_step):
+            return total, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
@@ -302,6 +328,7 @@ def main():
     if rank == 0:
         total_units = wl.units * args.steps * world
         achieved = wl.bytes / (kern_ms * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(args.config, wl.per_step)
         line = {
             "metric": METRIC,
             "value": total_units / tmax,
@@ -318,7 +345,8 @@ def main():
                     "resident in HBM before timing",
             "config": wl.config(world),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": tsrc,
                          "kernel": wl.kernel, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": wl.bytes, "bytes_model": wl.bytes_note},
             "cpu_baseline": cpu,

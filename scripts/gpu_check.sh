@@ -21,7 +21,15 @@ for s in $STEPS; do
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     tests) step pytest_gpu 1500 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} ; [ $? -le 1 ] || exit 1 ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} || exit $? ;;
-    prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} || exit $? ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu-baseline ${BENCH_ARGS:-} || exit $?
+           python scripts/trace_mean.py $OUT/prof 50 > $OUT/prof/timed_mean.txt; cat $OUT/prof/timed_mean.txt ;;
+    traffic)
+      for c in ${TRAFFIC_CFGS:-c2 c3 c4 c5}; do
+        for ctr in FETCH_SIZE WRITE_SIZE; do
+          step pmc_${c}_$ctr 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/pmc_${c}_$ctr -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline || exit $?
+        done
+        python scripts/pmc_traffic.py $c $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/pmc_traffic.json || exit 1
+      done ;;
     sweep) step sweep 600 python scripts/cwt_sweep.py || exit $? ;;
     diag)  step diag 600 python scripts/cwt_diag.py --mode seq || exit $? ;;
     counters) step counters 300 rocprofv3 -L ;;
