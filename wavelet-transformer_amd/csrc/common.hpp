@@ -22,6 +22,32 @@ __device__ __forceinline__ cpx cconj(cpx a) { return a * cpx{1.f, -1.f}; }
 __device__ __forceinline__ cpx cscale(cpx a, float s) { return a * s; }
 __device__ __forceinline__ float cabs2(cpx a) { return fmaf(a.x, a.x, a.y * a.y); }
 
+// Wave-uniform buffer resource for one output/input row (T8/T20 of the CDNA guide):
+// rows are addressed as SGPR descriptor + 32-bit per-lane voffset + SGPR soffset, so a
+// 16-position-per-thread row store needs one offset VGPR instead of 16 64-bit address
+// pairs (which the FFT kernels otherwise keep live across the scale loop).  The
+// pointer must be wave-uniform; readfirstlane makes that provable to the compiler.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+  const unsigned long long u = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(u));
+  const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(u >> 32));
+  void* q = reinterpret_cast<void*>((static_cast<unsigned long long>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, 0x7fffffff, 0x00020000);
+}
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_st(cpx v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, 0);
+}
+__device__ __forceinline__ float buf_ld_f32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ cpx buf_ld_c64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(cpx, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
 // Error codes returned by the C ABI (0 = success; >0 = hipError_t of the launch).
 enum : int {
   kOk = 0,

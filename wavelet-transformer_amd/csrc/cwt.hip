@@ -25,6 +25,32 @@ __device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, 
   float* ps_ = (KIND & kOutSig) ? a.out_sig + rowbase : nullptr;
   float* pu_ = (KIND & kOutUV) ? a.out_u + rowbase : nullptr;
   float* pv_ = (KIND & kOutUV) ? a.out_v + rowbase : nullptr;
+  // Full rows whose owner is a whole wave (NT >= 64 -> the row, hence rowbase, is
+  // wave-uniform) go through buffer stores: SGPR row base + one voffset VGPR.
+  constexpr bool kBuf = P::NT >= kWave;
+  if constexpr (FULL && kBuf) {
+    __amdgpu_buffer_rsrc_t rw, rp, rs, ru, rv;
+    if constexpr (KIND & kOutW) rw = uniform_rsrc(pw_);
+    if constexpr (KIND & kOutPow) rp = uniform_rsrc(pp_);
+    if constexpr (KIND & kOutSig) rs = uniform_rsrc(ps_);
+    if constexpr (KIND & kOutUV) {
+      ru = uniform_rsrc(pu_);
+      rv = uniform_rsrc(pv_);
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if constexpr (KIND & kOutW) buf_st(v[m], rw, 8 * t, 8 * m * P::NT);
+      const float pw = cabs2(v[m]);
+      if constexpr (KIND & kOutPow) buf_st(pw, rp, 4 * t, 4 * m * P::NT);
+      if constexpr (KIND & kOutSig) buf_st(pw * sg, rs, 4 * t, 4 * m * P::NT);
+      if constexpr (KIND & kOutUV) {
+        const float r = sqrtf(pw);
+        buf_st(r > 0.f ? v[m].y / r : 0.f, ru, 4 * t, 4 * m * P::NT);
+        buf_st(r > 0.f ? v[m].x / r : 1.f, rv, 4 * t, 4 * m * P::NT);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const int pos = t + m * P::NT;
@@ -54,8 +80,6 @@ __device__ __forceinline__ void store_any(const cpx (&v)[16], const CwtArgs& a, 
   }
 }
 
-constexpr int kMaxChunk = 512;  // per-workgroup scale-parameter table in LDS
-
 template <int LOGN, int NBUF, int MODE>
 __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 : CwtGeom<LOGN, MODE>::MINW)) cwt_morlet_kernel(CwtArgs a) {
   using P = FftPlan<LOGN>;
@@ -63,8 +87,10 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
   // per-scale table (alpha, log2 c, 1/signif, -) in LDS: the scale loop must not issue
   // global loads -- a load's vmcnt wait would also wait for every store of the
   // previous row (loads and stores retire in order on the same counter).
-  __shared__ cpx lds[NBUF * G::ROWS * P::PADN + 2 * kMaxChunk];
-  float4* prm_tab = reinterpret_cast<float4*>(lds + NBUF * G::ROWS * P::PADN);
+  __shared__ float4 lds4[(NBUF * G::ROWS * P::PADN) / 2 + G::MAXCHUNK + G::TWL_F4];
+  cpx* lds = reinterpret_cast<cpx*>(lds4);
+  float4* prm_tab = lds4 + (NBUF * G::ROWS * P::PADN) / 2;
+  float4* twl = prm_tab + G::MAXCHUNK;
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = tid - g * P::NT;
@@ -82,17 +108,24 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
     prm_tab[i] = make_float4(mp.x, mp.y, sg, 0.f);
   }
 
-  cpx tw[P::NTW_ALLOC];
-  fft_twiddles<LOGN>(tw, t);
+  constexpr bool TWL = G::TWL;
+  cpx tw[TWL ? P::NTW_REG : P::NTW_ALLOC];
+  if constexpr (TWL) {
+    fft_twiddle_table<LOGN>(twl, tid, G::BLOCK);
+    fft_twiddles_tail<LOGN>(tw, t);
+    __syncthreads();
+  } else {
+    fft_twiddles<LOGN>(tw, t);
+  }
   int par = 0;
 
   cpx X[16];
   load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
-  fft_row<LOGN, -1, NBUF>(X, my, bufstride, tw, t, par);
+  fft_row<LOGN, -1, NBUF, TWL>(X, my, bufstride, tw, t, par, twl);
   cpx X2[MODE == 1 ? 16 : 1];
   if constexpr (MODE == 1) {
     load_series<LOGN>(X2, a.x2, a.affine2, b, a.ld, a.n0, t);
-    fft_row<LOGN, -1, NBUF>(X2, my, bufstride, tw, t, par);
+    fft_row<LOGN, -1, NBUF, TWL>(X2, my, bufstride, tw, t, par, twl);
   }
   __syncthreads();  // prm_tab visible (the FFT barriers may be absent for N = 16)
 
@@ -108,13 +141,13 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
     const cpx prm = mkc(prm4.x, prm4.y);
     cpx v[16];
     morlet_filter<LOGN>(v, X, prm, f0, t);
-    fft_row<LOGN, 1, NBUF>(v, my, bufstride, tw, t, par);
+    fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
     if constexpr (MODE == 1) {
       cpx w1[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) w1[m] = v[m];
       morlet_filter<LOGN>(v, X2, prm, f0, t);
-      fft_row<LOGN, 1, NBUF>(v, my, bufstride, tw, t, par);
+      fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
 #pragma unroll
       for (int m = 0; m < 16; ++m) v[m] = cmul(w1[m], cconj(v[m]));
     }
@@ -210,7 +243,7 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
   int chunk = (a.S + nch - 1) / nch;
   chunk = ((chunk + rows - 1) / rows) * rows;
-  if (chunk > kMaxChunk) chunk = kMaxChunk;
+  if (chunk > G::MAXCHUNK) chunk = G::MAXCHUNK;
   nch = (a.S + chunk - 1) / chunk;
   a.nchunks = nch;
   a.chunk = chunk;

@@ -34,10 +34,16 @@ struct CwtGeom {
   using P = FftPlan<LOGN>;
   static constexpr int ROWS = P::NT >= 256 ? 1 : 256 / P::NT;
   static constexpr int BLOCK = P::NT * ROWS;
-  // waves per SIMD requested from the register allocator: 3 -> <= 168 VGPRs
-  // (3 workgroups of 256 per CU), 2 -> <= 256.  A 1024-thread block is 4 waves
-  // per SIMD by itself.
-  static constexpr int MINW = BLOCK >= 1024 ? 4 : (BLOCK >= 512 ? 2 : (MODE == 0 ? 3 : 2));
+  // LOGN >= 13 keeps the radix-16 twiddles in an LDS table (FftPlan::TWL_E): that is
+  // what brings the single-series kernel to <= 128 VGPRs, i.e. two 512-thread
+  // workgroups per CU (LDS 2 x 80 KiB) instead of one.
+  static constexpr bool TWL = LOGN >= 13;
+  // waves per SIMD requested from the register allocator (4 -> <= 128 VGPRs,
+  // 3 -> <= 168, 2 -> <= 256).  A 1024-thread block is 4 waves per SIMD by itself.
+  static constexpr int MINW = BLOCK >= 1024 ? 4 : (MODE == 1 ? 2 : (BLOCK >= 512 ? 4 : 3));
+  // scales per workgroup (size of the per-scale parameter table in LDS)
+  static constexpr int MAXCHUNK = 128;
+  static constexpr int TWL_F4 = TWL ? P::TWL_FLOAT4 : 0;
 };
 
 template <int LOGN>

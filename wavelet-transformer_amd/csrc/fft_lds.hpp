@@ -138,12 +138,25 @@ struct FftPlan {
   static constexpr int REM = 1 << (LOGN % 4);    // trailing radix (1 = none)
   static constexpr int NPASS = P16 + (REM > 1 ? 1 : 0);
   static constexpr int PADN = N + N / 16;        // padded LDS row length (complex)
-  // cached base twiddles per thread: w, w^2, w^4, w^8 per radix-16 pass >= 1,
-  // plus the trailing pass's per-butterfly bases.
-  static constexpr int NTW_REM = REM == 2 ? 8 : (REM == 4 ? 8 : (REM == 8 ? 6 : 0));
+  // cached base twiddles per thread: w, w^2, w^4, w^8 per radix-16 pass >= 1.  The
+  // trailing radix-R pass: butterfly q (q = 0..16/R-1) of thread t has twiddle base
+  // k = t + q*NT, and exp(2 pi i k/N) = exp(2 pi i t/N) * exp(2 pi i q/16): only the
+  // powers w_t, w_t^2, w_t^4 (R = 2, 4, 8 -> 1, 2, 3 bases) are kept, the q-rotation is
+  // a compile-time constant.
+  static constexpr int NTW_REM = REM == 2 ? 1 : (REM == 4 ? 2 : (REM == 8 ? 3 : 0));
   static constexpr int NTW = (P16 - 1) * 4 + NTW_REM;
   static constexpr int NTW_ALLOC = NTW > 0 ? NTW : 1;
+  // Alternative placement (TWL = true): the radix-16 bases of passes >= 1 live in a
+  // per-workgroup LDS table instead of 8 registers per pass.  Pass p (ns = 16^p) has
+  // ns entries k = t mod ns; the table holds (w, w^2) at [k] and (w^4, w^8) at
+  // [TWL_E + k], 16-byte entries so that consecutive lanes read conflict-free.
+  static constexpr int TWL_E = P16 >= 3 ? 16 + 256 : (P16 == 2 ? 16 : 0);
+  static constexpr int TWL_FLOAT4 = 2 * TWL_E;
+  static constexpr int NTW_REG = NTW_REM > 0 ? NTW_REM : 1;  // registers left with TWL
 };
+
+// Offset of pass p's entries in the LDS twiddle table.
+__host__ __device__ constexpr int twl_base(int p) { return p <= 1 ? 0 : 16; }
 
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
@@ -172,21 +185,32 @@ __device__ __forceinline__ void fft_twiddles(cpx* tw, int t) {
   }
   if constexpr (P::REM > 1) {
     constexpr int base = 4 * (P::P16 - 1);
-    constexpr int R = P::REM;
 #pragma unroll
-    for (int q = 0; q < 16 / R; ++q) {
-      const long long k = t + q * P::NT;
-      if constexpr (R == 2) {
-        tw[base + q] = expi_frac(k, P::N);
-      } else if constexpr (R == 4) {
-        tw[base + 2 * q + 0] = expi_frac(k, P::N);
-        tw[base + 2 * q + 1] = expi_frac(2 * k, P::N);
-      } else {
-        tw[base + 3 * q + 0] = expi_frac(k, P::N);
-        tw[base + 3 * q + 1] = expi_frac(2 * k, P::N);
-        tw[base + 3 * q + 2] = expi_frac(4 * k, P::N);
-      }
-    }
+    for (int e = 0; e < P::NTW_REM; ++e) tw[base + e] = expi_frac(static_cast<long long>(t) << e, P::N);
+  }
+}
+
+// TWL variant: the trailing-pass bases only (registers), see FftPlan::TWL_E.
+template <int LOGN>
+__device__ __forceinline__ void fft_twiddles_tail(cpx* tw, int t) {
+  using P = FftPlan<LOGN>;
+  if constexpr (P::REM > 1) {
+#pragma unroll
+    for (int e = 0; e < P::NTW_REM; ++e) tw[e] = expi_frac(static_cast<long long>(t) << e, P::N);
+  }
+}
+
+// Fill the LDS twiddle table (all threads of the workgroup; caller syncs before use).
+template <int LOGN>
+__device__ __forceinline__ void fft_twiddle_table(float4* tab, int tid, int nthreads) {
+  using P = FftPlan<LOGN>;
+  for (int i = tid; i < P::TWL_E; i += nthreads) {
+    const long long M = i < 16 ? 256 : 4096;  // pass 1: 16 * 16, pass 2: 256 * 16
+    const long long k = i < 16 ? i : i - 16;
+    const cpx w1 = expi_frac(k, M), w2 = expi_frac(2 * k, M);
+    const cpx w4 = expi_frac(4 * k, M), w8 = expi_frac(8 * k, M);
+    tab[i] = make_float4(w1.x, w1.y, w2.x, w2.y);
+    tab[P::TWL_E + i] = make_float4(w4.x, w4.y, w8.x, w8.y);
   }
 }
 
@@ -203,9 +227,11 @@ __device__ __forceinline__ cpx opaque(cpx w) {
 
 // v[r] *= w^r for r = 1..15 from the bases w, w^2, w^4, w^8.
 template <int DIR>
-__device__ __forceinline__ void apply_tw16(cpx* v, const cpx* b) {
-  const cpx w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
-  const cpx w4 = twd<DIR>(opaque(b[2])), w8 = twd<DIR>(opaque(b[3]));
+__device__ __forceinline__ void apply_tw16_w(cpx* v, cpx w1, cpx w2, cpx w4, cpx w8) {
+  w1 = twd<DIR>(w1);
+  w2 = twd<DIR>(w2);
+  w4 = twd<DIR>(w4);
+  w8 = twd<DIR>(w8);
   const cpx w3 = cmul(w1, w2), w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
   v[1] = cmul(v[1], w1);
   v[2] = cmul(v[2], w2);
@@ -224,18 +250,37 @@ __device__ __forceinline__ void apply_tw16(cpx* v, const cpx* b) {
   v[15] = cmul(v[15], cmul(w8, w7));
 }
 
-template <int R, int DIR>
-__device__ __forceinline__ void apply_tw_small(cpx* v, const cpx* b) {
+template <int DIR>
+__device__ __forceinline__ void apply_tw16(cpx* v, const cpx* b) {
+  apply_tw16_w<DIR>(v, opaque(b[0]), opaque(b[1]), opaque(b[2]), opaque(b[3]));
+}
+
+// Same from the LDS table: entry k of pass p.  The asm barrier keeps the two reads
+// inside the caller's loop (their LDS region is never written, so LICM would
+// otherwise hoist them and keep the 8 values live in registers).
+template <int DIR, int E>
+__device__ __forceinline__ void apply_tw16_lds(cpx* v, const float4* tab, int idx) {
+  asm volatile("" : "+v"(idx));
+  const float4 a = tab[idx], b = tab[E + idx];
+  apply_tw16_w<DIR>(v, mkc(a.x, a.y), mkc(a.z, a.w), mkc(b.x, b.y), mkc(b.z, b.w));
+}
+
+// Trailing radix-R pass, butterfly Q: v[r] *= (w_t * exp(2 pi i Q/16))^r, r = 1..R-1, from
+// the bases b = (w_t, w_t^2, w_t^4) (inverse sign; DIR < 0 conjugates).
+template <int R, int DIR, int Q>
+__device__ __forceinline__ void apply_tw_tail(cpx* v, const cpx* b) {
   if constexpr (R == 2) {
-    v[1] = cmul(v[1], twd<DIR>(b[0]));
+    v[1] = cmul(v[1], rot16<DIR, Q>(twd<DIR>(opaque(b[0]))));
   } else if constexpr (R == 4) {
-    const cpx w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
+    const cpx w1 = rot16<DIR, Q>(twd<DIR>(opaque(b[0])));
+    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(opaque(b[1])));
     v[1] = cmul(v[1], w1);
     v[2] = cmul(v[2], w2);
     v[3] = cmul(v[3], cmul(w1, w2));
   } else {
-    const cpx w1 = twd<DIR>(opaque(b[0])), w2 = twd<DIR>(opaque(b[1]));
-    const cpx w4 = twd<DIR>(opaque(b[2]));
+    const cpx w1 = rot16<DIR, Q>(twd<DIR>(opaque(b[0])));
+    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(opaque(b[1])));
+    const cpx w4 = rot16<DIR, 4 * Q>(twd<DIR>(opaque(b[2])));
     const cpx w3 = cmul(w1, w2);
     v[1] = cmul(v[1], w1);
     v[2] = cmul(v[2], w2);
@@ -247,14 +292,24 @@ __device__ __forceinline__ void apply_tw_small(cpx* v, const cpx* b) {
   }
 }
 
+template <int R, int DIR, int Q>
+__device__ __forceinline__ void tail_butterflies(cpx* v, const cpx* b) {
+  if constexpr (Q > 0) {
+    tail_butterflies<R, DIR, Q - 1>(v, b);
+    apply_tw_tail<R, DIR, Q - 1>(v + (Q - 1) * R, b);
+    dft_small<R, DIR>(v + (Q - 1) * R);
+  }
+}
+
 // In-place FFT of one row.  v[m] holds position t + m*NT on entry and exit.
 // lds: this row's region of buffer 0; bufstride: offset (in cpx) of buffer 1
 // when NBUF == 2.  par: running buffer parity (NBUF == 2), shared by all calls of
 // the workgroup in the same order.  Every thread of the workgroup must call this
 // the same number of times (it contains __syncthreads()).
-template <int LOGN, int DIR, int NBUF>
+template <int LOGN, int DIR, int NBUF, bool TWL = false>
 __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int bufstride,
-                                        const cpx* tw, int t, int& par) {
+                                        const cpx* tw, int t, int& par,
+                                        const float4* twl = nullptr) {
   using P = FftPlan<LOGN>;
   constexpr bool kAligned = (P::NT % 16) == 0;  // strides are multiples of 16 -> pad is additive
   dft16<DIR>(v);
@@ -283,7 +338,10 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
         for (int r = 0; r < 16; ++r) v[r] = rbuf[lpad(t + r * P::NT)];
       }
       if constexpr (NBUF == 2) par ^= 1;
-      apply_tw16<DIR>(v, tw + 4 * (p - 1));
+      if constexpr (TWL)
+        apply_tw16_lds<DIR, P::TWL_E>(v, twl, twl_base(p) + (t & (ns - 1)));
+      else
+        apply_tw16<DIR>(v, tw + 4 * (p - 1));
       dft16<DIR>(v);
       if (!last) {
         cpx* wbuf = lds + (NBUF == 2 ? par * bufstride : 0);
@@ -298,8 +356,7 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
     } else {
       constexpr int R = P::REM > 1 ? P::REM : 16;
       constexpr int Q = 16 / R;
-      constexpr int tb = 4 * (P::P16 - 1);
-      constexpr int tstep = R == 2 ? 1 : (R == 4 ? 2 : 3);
+      constexpr int tb = TWL ? 0 : 4 * (P::P16 - 1);
 #pragma unroll
       for (int q = 0; q < Q; ++q)
 #pragma unroll
@@ -312,11 +369,7 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
           }
         }
       if constexpr (NBUF == 2) par ^= 1;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        apply_tw_small<R, DIR>(v + q * R, tw + tb + tstep * q);
-        dft_small<R, DIR>(v + q * R);
-      }
+      tail_butterflies<R, DIR, Q>(v, tw + tb);
       // register q*R + r holds position t + (q + r*Q)*NT
       cpx o[16];
 #pragma unroll

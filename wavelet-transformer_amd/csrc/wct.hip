@@ -25,15 +25,21 @@ struct WctGeom {
   using P = FftPlan<LOGN>;
   static constexpr int ROWS = P::NT >= 256 ? 1 : 256 / P::NT;
   static constexpr int BLOCK = P::NT * ROWS;
-  static constexpr int MINW = BLOCK >= 1024 ? 4 : (BLOCK >= 512 ? 2 : 2);
+  // as CwtGeom: LDS twiddle table from LOGN 13 on, so that phase A fits 128 VGPRs and
+  // two 512-thread workgroups share a CU
+  static constexpr bool TWL = LOGN >= 13;
+  static constexpr int MINW = BLOCK >= 512 ? 4 : 2;
+  static constexpr int MAXCHUNK = 128;
+  static constexpr int TWL_F4 = TWL ? P::TWL_FLOAT4 : 0;
 };
-
-constexpr int kWctMaxChunk = 512;
 
 // bins this thread owns: kk = t + (m < 8 ? m : m - 16) * NT
 template <int LOGN>
 __device__ __forceinline__ void smooth_filter(cpx (&v)[16], float beta, float scale, int t) {
   using P = FftPlan<LOGN>;
+  // kk^2 is loop-invariant in the caller's scale loop: without the barrier the
+  // compiler hoists all 16 and spills them
+  asm volatile("" : "+v"(t));
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const float kk = static_cast<float>(t + (m < 8 ? m : m - 16) * P::NT);
@@ -76,19 +82,49 @@ __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, c
 template <int LOGN>
 __device__ __forceinline__ void load_spec(cpx (&X)[16], const cpx* row, int t) {
   using P = FftPlan<LOGN>;
-  asm volatile("" : "+s"(row));
+  if constexpr (P::NT >= kWave) {
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row);
+    int voff = 8 * t;
+    asm volatile("" : "+v"(voff));
 #pragma unroll
-  for (int m = 0; m < 16; ++m) X[m] = row[t + m * P::NT];
+    for (int m = 0; m < 16; ++m) X[m] = buf_ld_c64(r, voff, 8 * m * P::NT);
+  } else {
+    asm volatile("" : "+s"(row));
+#pragma unroll
+    for (int m = 0; m < 16; ++m) X[m] = row[t + m * P::NT];
+  }
 }
 
-template <int LOGN>
+// Row store of 16 positions per thread.  BUF (full rows owned by whole waves): buffer
+// stores off a wave-uniform row base, no per-position address registers; otherwise
+// plain stores masked to pos < n0.
+template <int LOGN, bool BUF, typename T, typename F>
+__device__ __forceinline__ void put_row(T* row, int t, int n0, F&& val) {
+  using P = FftPlan<LOGN>;
+  if constexpr (BUF) {
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) buf_st(val(m), r, static_cast<int>(sizeof(T)) * t, static_cast<int>(sizeof(T)) * m * P::NT);
+  } else {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int pos = t + m * P::NT;
+      if (pos < n0) row[pos] = val(m);
+    }
+  }
+}
+
+template <int LOGN, bool FULL>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  __shared__ cpx lds[G::ROWS * P::PADN + 2 * kWctMaxChunk];
+  constexpr bool BUF = FULL && P::NT >= kWave;
+  __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::MAXCHUNK + G::TWL_F4];
+  cpx* lds = reinterpret_cast<cpx*>(lds4);
   cpx* prm_tab = lds + G::ROWS * P::PADN;      // (alpha, log2 c) of the Morlet filter
-  cpx* smt_tab = prm_tab + kWctMaxChunk;       // (beta, 1/(N s)) of the time smoother
+  cpx* smt_tab = prm_tab + G::MAXCHUNK;        // (beta, 1/(N s)) of the time smoother
+  float4* twl = lds4 + (G::ROWS * P::PADN) / 2 + G::MAXCHUNK;
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = tid - g * P::NT;
@@ -109,12 +145,19 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     smt_tab[i] = mkc(static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn),
                              static_cast<float>(1.0 / (static_cast<double>(P::N) * s)));
   }
-  cpx tw[P::NTW_ALLOC];
-  fft_twiddles<LOGN>(tw, t);
+  constexpr bool TWL = G::TWL;
+  cpx tw[TWL ? P::NTW_REG : P::NTW_ALLOC];
+  if constexpr (TWL) {
+    fft_twiddle_table<LOGN>(twl, tid, G::BLOCK);
+    fft_twiddles_tail<LOGN>(tw, t);
+  } else {
+    fft_twiddles<LOGN>(tw, t);
+  }
   int par = 0;
   __syncthreads();
 
   const float f0 = static_cast<float>(a.f0);
+  const int n0 = a.n0;
   const int iters = (j1 - j0 + G::ROWS - 1) / G::ROWS;
   for (int it = 0; it < iters; ++it) {
     const int jl = it * G::ROWS + g;
@@ -124,60 +167,51 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     cpx w1[16], v[16];
     load_spec<LOGN>(w1, spec1, t);
     morlet_filter<LOGN>(v, w1, prm, f0, t);
-    fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
+    fft_row<LOGN, 1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
 #pragma unroll
     for (int m = 0; m < 16; ++m) w1[m] = v[m];
     load_spec<LOGN>(v, spec2, t);
     morlet_filter<LOGN>(v, v, prm, f0, t);
-    fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
+    fft_row<LOGN, 1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
     const int j = j0 + jl;
-    const long long rowbase = (b * a.S + (valid ? j : j0)) * static_cast<long long>(a.n0);
-    float* urow = valid && a.out_u ? a.out_u + rowbase : nullptr;
-    float* vrow = valid && a.out_v ? a.out_v + rowbase : nullptr;
-    float* prow = valid && a.out_pow ? a.out_pow + rowbase : nullptr;
-    float* arow = valid && a.out_sig ? a.out_sig + rowbase : nullptr;  // phase angle
-    // W12 -> |W12|^2, angle, arrows; then z1 = |W1|^2 + i |W2|^2 and z2 = W12 (zero
-    // past n0: the reference smooths the row zero-padded to N)
+    const long long rowbase = (b * a.S + (valid ? j : j0)) * static_cast<long long>(n0);
+    // W12 = W1 conj(W2) -> |W12|^2, angle, arrows (rows of invalid groups are not
+    // stored); then z1 = |W1|^2 + i |W2|^2 and W12, zero past n0 (the reference
+    // smooths the row zero-padded to N)
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int pos = t + m * P::NT;
       const cpx w12 = cmul(w1[m], cconj(v[m]));
-      const bool in = pos < a.n0;
-      if (in) {
-        const float p2 = cabs2(w12);
-        if (prow) prow[pos] = p2;
-        if (arow) arow[pos] = atan2f(w12.y, w12.x);
-        if (urow) {
-          const float r = sqrtf(p2);
-          urow[pos] = r > 0.f ? w12.y / r : 0.f;
-          vrow[pos] = r > 0.f ? w12.x / r : 1.f;
-        }
-      }
       const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
+      const bool in = FULL || pos < n0;
       w1[m] = in ? w12 : mkc(0.f, 0.f);
       v[m] = in ? z1 : mkc(0.f, 0.f);
     }
-    fft_row<LOGN, -1, 1>(v, my, bufstride, tw, t, par);
+    fft_row<LOGN, -1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
     smooth_filter<LOGN>(v, smt.x, smt.y, t);
-    fft_row<LOGN, 1, 1>(v, my, bufstride, tw, t, par);
+    fft_row<LOGN, 1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
+    // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
+    if (valid) put_row<LOGN, BUF>(TA + rowbase, t, n0, [&](int m) { return v[m]; });
+    // the XWT-shaped outputs once z1 is dead (only W12 live: no spills around atan2)
     if (valid) {
-      cpx* ta = TA + rowbase;
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const int pos = t + m * P::NT;
-        if (pos < a.n0) ta[pos] = v[m];  // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
+      if (a.out_pow) put_row<LOGN, BUF>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w1[m]); });
+      if (a.out_sig)  // phase angle
+        put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return atan2f(w1[m].y, w1[m].x); });
+      if (a.out_u) {
+        put_row<LOGN, BUF>(a.out_u + rowbase, t, n0, [&](int m) {
+          const float r = sqrtf(cabs2(w1[m]));
+          return r > 0.f ? w1[m].y / r : 0.f;
+        });
+        put_row<LOGN, BUF>(a.out_v + rowbase, t, n0, [&](int m) {
+          const float r = sqrtf(cabs2(w1[m]));
+          return r > 0.f ? w1[m].x / r : 1.f;
+        });
       }
     }
-    fft_row<LOGN, -1, 1>(w1, my, bufstride, tw, t, par);
+    fft_row<LOGN, -1, 1, TWL>(w1, my, bufstride, tw, t, par, twl);
     smooth_filter<LOGN>(w1, smt.x, smt.y, t);
-    fft_row<LOGN, 1, 1>(w1, my, bufstride, tw, t, par);
-    if (!valid) continue;
-    cpx* tb = TB + rowbase;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int pos = t + m * P::NT;
-      if (pos < a.n0) tb[pos] = w1[m];  // smoothed W12/s
-    }
+    fft_row<LOGN, 1, 1, TWL>(w1, my, bufstride, tw, t, par, twl);
+    if (valid) put_row<LOGN, BUF>(TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
   }
 }
 
@@ -252,13 +286,16 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, hipStream_t s
   if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
   int chunk = (a.S + nch - 1) / nch;
   chunk = ((chunk + rows - 1) / rows) * rows;
-  if (chunk > kWctMaxChunk) chunk = kWctMaxChunk;
+  if (chunk > G::MAXCHUNK) chunk = G::MAXCHUNK;
   nch = (a.S + chunk - 1) / chunk;
   a.nchunks = nch;
   a.chunk = chunk;
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  hipLaunchKernelGGL(wct_phase_a<LOGN>, dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, TA, TB);
+  if (a.n0 == (1 << LOGN))
+    hipLaunchKernelGGL((wct_phase_a<LOGN, true>), dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, TA, TB);
+  else
+    hipLaunchKernelGGL((wct_phase_a<LOGN, false>), dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, TA, TB);
   return launch_status();
 }
 
