@@ -12,8 +12,8 @@ barrier and the max-over-ranks of the timed region.
 
 Rank 0 prints ONE JSON line: value = all ranks' coefficients / max-over-ranks time,
 plus "roofline" (dominant kernel, HIP-event timed on its own stream) and
-"cpu_baseline" (the fp64 oracle restatement of pycwt.cwt on a bounded sample, host
-cores of this box, N = 1 only).
+"cpu_baseline" (the fp64 oracle restatement of the config's reference path on a
+bounded sample, host cores of this box, N = 1 only).
 """
 
 from __future__ import annotations
@@ -50,36 +50,66 @@ def synth_batch(rng, B, n, dtype=np.float32):
 
 
 # ------------------------------------------------------------------ CPU baseline
+# The oracle restatements (test infrastructure, timed here as the CPU reference):
+#   c2 / c5  pycwt.cwt (scipy.fftpack, fp64) per series at the config's shape
+#   c3       src/modwt.py modwt + imodwt (scipy.ndimage.convolve1d on zero-stuffed
+#            dilated filters -- the reference's own algorithm, bitwise pinned)
+#   c4       pycwt.wct (sig=False) per pair, which also forms W12 for the XWT power
 def _cpu_worker(args):
-    seed, count, n0, dj, J = args
+    cfg, seed, count = args
     import os as _os
     _os.environ.setdefault("OMP_NUM_THREADS", "1")
-    from oracle import pycwt_spec as pc
     rng = np.random.default_rng(seed)
-    x = synth_batch(rng, count, n0).astype(np.float64)
+    if cfg in ("c2", "c5"):
+        from oracle import pycwt_spec as pc
+        wl = CONFIGS[cfg]
+        x = synth_batch(rng, count, wl.n0).astype(np.float64)
+        t0 = time.perf_counter()
+        for b in range(count):
+            S = pc.cwt(x[b], DT, wl.dj, 2 * DT, wl.J)[0].shape[0]
+        return time.perf_counter() - t0, count * S * wl.n0
+    if cfg == "c3":
+        from oracle import modwt_spec as ms
+        from wtmi.wavelets import Wavelet
+        w = Wavelet("db4")
+        x = synth_batch(rng, count, C3.n)  # fp32 in -> fp32 out, as the reference
+        t0 = time.perf_counter()
+        for b in range(count):
+            ms.imodwt(ms.modwt(x[b], w.dec_lo, w.dec_hi, C3.J), w.dec_lo, w.dec_hi)
+        return time.perf_counter() - t0, count * (C3.J + 1) * C3.n
+    from oracle import pycwt_spec as pc
+    y1 = synth_batch(rng, count, C4.n).astype(np.float64)
+    y2 = 0.6 * np.roll(y1, 3, axis=1) + 0.8 * synth_batch(rng, count, C4.n)
     t0 = time.perf_counter()
-    S = 0
     for b in range(count):
-        W = pc.cwt(x[b], DT, dj, 2 * DT, J)[0]
-        S = W.shape[0]
-    return time.perf_counter() - t0, count * S * n0
+        S = pc.wct(y1[b], y2[b], DT, dj=C4.dj, s0=2 * DT, J=-1, sig=False)[0].shape[0]
+    return time.perf_counter() - t0, count * S * C4.n
 
 
-def cpu_baseline(n0, dj, J, per_worker, workers):
+CPU_SAMPLE = {"c2": "pycwt.cwt restatement (scipy.fftpack, fp64), series x 4096 samples x 128 scales",
+              "c5": "pycwt.cwt restatement (scipy.fftpack, fp64), series x 8192 samples x 256 scales",
+              "c3": "src/modwt.py modwt+imodwt restatement (scipy convolve1d, dilated db4, J=10), "
+                    "series x 16384 samples",
+              "c4": "pycwt.wct(sig=False) restatement (2 CWTs + 3 Morlet.smooth, fp64), "
+                    "pairs x 8192 samples x 97 scales"}
+CPU_PER_WORKER = {"c2": 32, "c5": 10, "c3": 2, "c4": 2}  # ~1 s per worker, ~16 s of CPU in all
+
+
+def cpu_baseline(cfg, per_worker, workers):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    jobs = [(7000 + i, per_worker, n0, dj, J) for i in range(workers)]
+    per_worker = per_worker or CPU_PER_WORKER[cfg]
+    jobs = [(cfg, 7000 + i, per_worker) for i in range(workers)]
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
         res = pool.map(_cpu_worker, jobs)
     wall = time.perf_counter() - t0
     busy = max(r[0] for r in res)
-    coeffs = sum(r[1] for r in res)
-    return {"value": coeffs / busy, "unit": "coeffs/s", "cores": workers, "kind": "port",
-            "sample": f"{workers * per_worker} series x {n0} samples x {J + 1} scales "
-                      f"(C2 shape), fp64 oracle restatement of pycwt.cwt (scipy.fftpack), "
-                      f"{workers} processes x {per_worker} series; rate = coeffs / slowest "
-                      f"worker's compute time (pool wall {wall:.1f} s)",
+    units = sum(r[1] for r in res)
+    return {"value": units / busy, "unit": "coeffs/s", "cores": workers, "kind": "port",
+            "sample": f"{workers * per_worker} x {CPU_SAMPLE[cfg]}; {workers} single-threaded "
+                      f"processes x {per_worker}; rate = coefficients / slowest worker's compute "
+                      f"time (pool wall {wall:.1f} s)",
             "single_core_value": res[0][1] / res[0][0]}
 
 
@@ -270,7 +300,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-workers", type=int, default=16)
-    ap.add_argument("--cpu-per-worker", type=int, default=32)
+    ap.add_argument("--cpu-per-worker", type=int, default=0, help="0 = per-config default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -280,10 +310,10 @@ def main():
     wl_cls = CONFIGS[args.config]
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c5"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before any GPU initialisation (spawned workers never touch the GPU)
         workers = max(1, min(args.cpu_workers, len(os.sched_getaffinity(0))))
-        cpu = cpu_baseline(C2.n0, C2.dj, C2.J, args.cpu_per_worker, workers)
+        cpu = cpu_baseline(args.config, args.cpu_per_worker, workers)
 
     import torch
     import torch.distributed as dist

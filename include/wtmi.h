@@ -67,6 +67,24 @@ int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long ba
                     float* out_coh, float* out_power, float* out_phase, float* out_u,
                     float* out_v, void* stream);
 
+/* ---- WCT Monte-Carlo significance (K10 / K11) ---------------------------------
+ * Replace the pieces of pycwt.wct_significance reached from src/wct.py:106-118 with
+ * sig=True.
+ * wtmi_rednoise: helpers.rednoise(n, g, 1) for `count` series into out[count][ld]:
+ *   y = lfilter([1,0],[1,-g], randn(n + tau))[tau:], tau = ceil(-2/ln|g|) (0 if g == 0).
+ *   Normals come from Philox4x32-10 keyed by `seed`; series c uses stream
+ *   first_series + c, so batches can be drawn in pieces reproducibly.
+ * wtmi_coherence_histogram: adds, for s < n_hist_scales, the counts of
+ *   clamp(floor(coh[p][s][t] * nbins), 0, nbins-1) over all pairs p and
+ *   t in [t_lo[s], t_hi[s]) (the points outside the cone of influence; t_lo/t_hi are
+ *   device int arrays) into hist[n_hist_scales][nbins] (uint32, caller-zeroed).
+ *   nbins <= 4096.                                                                  */
+int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g,
+                  unsigned long long seed, unsigned long long first_series, void* stream);
+int wtmi_coherence_histogram(const float* coh, long long batch, long long n0, int n_scales,
+                             const int* t_lo, const int* t_hi, int n_hist_scales, int nbins,
+                             unsigned int* hist, void* stream);
+
 /* ---- MODWT (K3 / K4) -----------------------------------------------------------
  * Replace src/modwt.py:126-144 (modwt: rows [W_1..W_J, V_J]) and :147-160 (imodwt).
  * dec_lo/dec_hi: HOST pointers to the n_taps analysis filters (pywt dec_lo/dec_hi);

@@ -26,6 +26,7 @@ Reference call sites (what these functions stand in for):
   * ``significance`` <- ``src/cwt.py:123-131``
   * ``xwt``          <- ``src/xwt.py:93-101``
   * ``wct``          <- ``src/wct.py:106-118``, ``src/xwt.py:122-134``
+  * ``wct_significance`` / ``rednoise`` <- inside ``wct(sig=True)``, ``src/wct.py:106-118``
 """
 
 from __future__ import annotations
@@ -241,12 +242,11 @@ def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95,
 
 def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
         wavelet=None, normalize=True, **kwargs):
-    """pycwt ``wct`` with ``sig=False``.
+    """pycwt ``wct``.
 
     ``**kwargs`` swallows ``cache=`` and ``delta_j=`` exactly as pycwt does
     (reference quirk B.5: ``src/xwt.py:126`` passes ``delta_j=`` and so runs at
-    the default dj=1/12).  The Monte-Carlo ``wct_significance`` (sig=True) is
-    SURVEY §8(f) row 1 and not restated here.
+    the default dj=1/12); ``mc_count`` / ``rng`` reach ``wct_significance``.
     """
     wavelet = wavelet or Morlet(6)
     if np.asarray(y1).size != np.asarray(y2).size:
@@ -263,5 +263,96 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
     WCT = np.abs(S12) ** 2 / (S1 * S2)
     aWCT = np.angle(W12)
     if sig:
-        raise NotImplementedError("wct_significance (Monte Carlo) is SURVEY 8(f) row 1")
-    return WCT, aWCT, coi, freq, np.asarray([0])
+        a1, _, _ = ar1(y1)
+        a2, _, _ = ar1(y2)
+        sig = wct_significance(a1, a2, dt=dt, dj=dj, s0=s0, J=J,
+                               significance_level=significance_level, wavelet=wavelet,
+                               **{k: v for k, v in kwargs.items() if k in ("mc_count", "rng")})
+    else:
+        sig = np.asarray([0])
+    return WCT, aWCT, coi, freq, sig
+
+
+# ------------------------------------------------------------ Monte-Carlo significance
+# pycwt 0.4.0b0 ``helpers.rednoise`` and ``wavelet.wct_significance`` (SURVEY A.5;
+# reached from src/wct.py:106-118 with sig=True).  The published algorithm draws from
+# the unseeded global ``np.random``; here the generator is a parameter so tests can
+# seed it.  Parity with the GPU path is statistical (different random streams).
+
+def rednoise(N: int, g: float, a: float = 1.0, rng=None) -> np.ndarray:
+    """AR(1) red noise: lfilter([1, 0], [1, -g], randn(N + tau) * a)[tau:], with the
+    burn-in tau = ceil(-2 / ln|g|) (twice the decorrelation time); white if g == 0."""
+    from scipy.signal import lfilter
+    rng = rng if rng is not None else np.random.default_rng()
+    if g == 0:
+        return (rng.standard_normal((N, 1)) * a).flatten()
+    tau = int(np.ceil(-2 / np.log(np.abs(g))))
+    yr = lfilter([1, 0], [1, -g], rng.standard_normal((N + tau, 1)) * a, axis=0)
+    return yr[tau:].flatten()
+
+
+def wct_sig_geometry(dt, dj, s0, J, wavelet=None):
+    """Noise length N = ceil(6 s0 2^(J dj) / dt), the outside-COI mask [J+1, N] and
+    maxscale (last scale with any point outside the COI), as in wct_significance."""
+    wavelet = wavelet or Morlet(6)
+    ms = s0 * (2 ** (J * dj)) / dt
+    N = int(np.ceil(ms * 6))
+    sj = s0 * 2 ** (np.arange(0, J + 1) * dj)
+    freq = 1 / (wavelet.flambda() * sj)
+    coi = N / 2 - np.abs(np.arange(0, N) - (N - 1) / 2)
+    coi = wavelet.flambda() * wavelet.coi() * dt * coi
+    period = np.ones([1, N]) / freq[:, None]
+    outsidecoi = period <= (np.ones([J + 1, 1]) * coi[None, :])
+    maxscale = int(np.nonzero(outsidecoi.any(axis=1))[0][-1])
+    return N, sj, outsidecoi, maxscale
+
+
+def coherence_histogram(R2, outsidecoi, maxscale, nbins=1000, wlc=None):
+    """One Monte-Carlo pass of the counter: for s < maxscale, bins floor(R2 * nbins)
+    of the points outside the COI.  (pycwt indexes with int(floor(..)); R2 == 1.0
+    exactly would raise IndexError there -- clamped to the last bin here.)"""
+    J1 = R2.shape[0]
+    wlc = np.zeros((J1, nbins)) if wlc is None else wlc
+    for s in range(maxscale):
+        cd = np.floor(R2[s, outsidecoi[s]] * nbins).astype(np.int64)
+        np.add.at(wlc[s], np.clip(cd, 0, nbins - 1), 1)
+    return wlc
+
+
+def significance_from_histogram(wlc, outsidecoi, maxscale, significance_level=0.95):
+    """sig95 from the per-scale counters: NaN for scales with points outside the COI,
+    then for s < maxscale the significance_level quantile interpolated on the
+    mid-bin coherence grid over the non-empty bins (P = (cumsum - 0.5) / total)."""
+    nbins = wlc.shape[1]
+    sig95 = np.zeros(wlc.shape[0])
+    sig95[outsidecoi.any(axis=1)] = np.nan
+    R2y = (np.arange(nbins) + 0.5) / nbins
+    for s in range(maxscale):
+        sel = wlc[s, :] != 0
+        P = wlc[s, sel].cumsum()
+        P = (P - 0.5) / P[-1]
+        sig95[s] = np.interp(significance_level, P, R2y[sel])
+    return sig95
+
+
+def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet=None,
+                     mc_count=300, rng=None, nbins=1000):
+    """pycwt ``wct_significance`` without the disk cache."""
+    wavelet = wavelet or Morlet(6)
+    rng = rng if rng is not None else np.random.default_rng()
+    N, sj, outsidecoi, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
+    scales = np.ones([1, N]) * sj[:, None]
+    wlc = np.zeros((J + 1, nbins))
+    kw = dict(dj=dj, s0=s0, J=J, wavelet=wavelet)
+    for _ in range(mc_count):
+        noise1 = rednoise(N, al1, 1, rng)
+        noise2 = rednoise(N, al2, 1, rng)
+        nW1, sj, _, _, _, _ = cwt(noise1, dt, **kw)
+        nW2, sj, _, _, _, _ = cwt(noise2, dt, **kw)
+        nW12 = nW1 * nW2.conj()
+        S1 = wavelet.smooth(np.abs(nW1) ** 2 / scales, dt, dj, sj)
+        S2 = wavelet.smooth(np.abs(nW2) ** 2 / scales, dt, dj, sj)
+        S12 = wavelet.smooth(nW12 / scales, dt, dj, sj)
+        R2 = np.abs(S12) ** 2 / (S1 * S2)
+        coherence_histogram(R2, outsidecoi, maxscale, nbins, wlc)
+    return significance_from_histogram(wlc, outsidecoi, maxscale, significance_level)

@@ -179,8 +179,12 @@ def test_src_xwt_and_wct():
     refw = gs.run_wct(y1, y2, wct.DT, wct.DJ, wct.S0)
     assert np.abs(rw.coherence - refw[0]).max() <= 1e-4
     assert np.isinf(rw.significance_levels).all() and np.isinf(refw[2]).all()  # quirk B.8
-    with pytest.raises(NotImplementedError):
-        wct.run_wct(dw, calculate_signficance=True)
+    # significance on: Monte-Carlo levels (test_gpu_wct_sig.py pins them statistically);
+    # the coherence is unchanged and the ratio is |coh| / sig95 per scale
+    rs = wct.run_wct(dw, calculate_signficance=True)
+    np.testing.assert_array_equal(rs.coherence, rw.coherence)
+    fin = np.isfinite(rs.significance_levels)
+    assert fin.any() and (rs.significance_levels[fin] > 0).all()
 
 
 def test_src_dwt_and_modwt(dwt_golden, modwt_golden):

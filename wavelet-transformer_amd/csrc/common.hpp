@@ -48,6 +48,15 @@ __device__ __forceinline__ cpx buf_ld_c64(__amdgpu_buffer_rsrc_t r, int voff, in
   return __builtin_bit_cast(cpx, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 
+// Bijective XCD-aware block remap (CDNA guide T1).  The dispatcher deals blocks
+// round-robin over the 8 XCDs, so b, b+8, b+16, ... share one XCD and its L2; this
+// hands each XCD a contiguous range of logical blocks, so blocks that read the same
+// data (e.g. the scale chunks of one series pair) run behind the same L2.
+__device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned nb) {
+  const unsigned x = bid & 7u, slot = bid >> 3, q = nb >> 3, r = nb & 7u;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+}
+
 // Error codes returned by the C ABI (0 = success; >0 = hipError_t of the launch).
 enum : int {
   kOk = 0,

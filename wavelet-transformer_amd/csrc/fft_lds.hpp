@@ -9,9 +9,12 @@
 // registers across many inverse transforms (the per-scale CWT loop) and stores are
 // coalesced (consecutive lanes -> consecutive samples).
 //
-// LDS rows are padded by one complex per 16 (index i -> i + i/16) so that the
-// radix-16 scatter of pass 0 (lane stride 16 complex) is bank-conflict free for
-// ds_write_b64.  DIR = -1 forward, +1 inverse; the transform is unnormalised.
+// LDS rows are padded by one complex per 32 (index i -> i + i/32).  The gather of
+// every pass >= 1 reads 32 consecutive positions per 32-lane ds_read_b64 group, which
+// then sit in one 32-slot block and cover the 64 banks once (a 1-per-16 pad put lane 31
+// on lane 0's banks: a 2-way conflict on every read, +50 % LDS cycles).  The price is
+// a 2-way conflict on pass 0's stride-16 scatter only (lanes 2k, 2k+1 of a 16-lane
+// ds_write group).  DIR = -1 forward, +1 inverse; the transform is unnormalised.
 #pragma once
 
 #include "common.hpp"
@@ -137,7 +140,7 @@ struct FftPlan {
   static constexpr int P16 = LOGN / 4;           // radix-16 passes
   static constexpr int REM = 1 << (LOGN % 4);    // trailing radix (1 = none)
   static constexpr int NPASS = P16 + (REM > 1 ? 1 : 0);
-  static constexpr int PADN = N + N / 16;        // padded LDS row length (complex)
+  static constexpr int PADN = N + N / 32 + ((N / 32) & 1);  // padded row (complex, even)
   // cached base twiddles per thread: w, w^2, w^4, w^8 per radix-16 pass >= 1.  The
   // trailing radix-R pass: butterfly q (q = 0..16/R-1) of thread t has twiddle base
   // k = t + q*NT, and exp(2 pi i k/N) = exp(2 pi i t/N) * exp(2 pi i q/16): only the
@@ -158,7 +161,7 @@ struct FftPlan {
 // Offset of pass p's entries in the LDS twiddle table.
 __host__ __device__ constexpr int twl_base(int p) { return p <= 1 ? 0 : 16; }
 
-__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 5); }
 
 // exp(+2 pi i num / den), correctly rounded from double.
 __device__ __forceinline__ cpx expi_frac(long long num, long long den) {
@@ -311,13 +314,13 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
                                         const cpx* tw, int t, int& par,
                                         const float4* twl = nullptr) {
   using P = FftPlan<LOGN>;
-  constexpr bool kAligned = (P::NT % 16) == 0;  // strides are multiples of 16 -> pad is additive
+  constexpr bool kAligned = (P::NT % 32) == 0;  // strides are multiples of 32 -> pad is additive
   dft16<DIR>(v);
   if constexpr (P::NPASS == 1) return;
   {
     cpx* buf = lds + (NBUF == 2 ? par * bufstride : 0);
     if constexpr (NBUF == 1) __syncthreads();
-    cpx* w = buf + 17 * t;  // lpad(16 t + r) = 17 t + r
+    cpx* w = buf + 16 * t + (t >> 1);  // lpad(16 t + r) = 16 t + t/2 + r  (r < 16)
 #pragma unroll
     for (int r = 0; r < 16; ++r) w[r] = v[r];
     __syncthreads();
@@ -332,7 +335,7 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
       if constexpr (kAligned) {
         const cpx* rb = rbuf + pt;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = rb[r * (P::NT + P::NT / 16)];
+        for (int r = 0; r < 16; ++r) v[r] = rb[r * (P::NT + P::NT / 32)];
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = rbuf[lpad(t + r * P::NT)];
@@ -347,9 +350,14 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
         cpx* wbuf = lds + (NBUF == 2 ? par * bufstride : 0);
         const int idxD = (t / ns) * ns * 16 + (t & (ns - 1));
         if constexpr (NBUF == 1) __syncthreads();
-        cpx* wb = wbuf + lpad(idxD);  // ns >= 16 -> r*ns keeps the pad additive
+        cpx* wb = wbuf + lpad(idxD);
+        if (ns >= 32) {  // r*ns is a multiple of 32: the pad is additive
 #pragma unroll
-        for (int r = 0; r < 16; ++r) wb[r * (ns + ns / 16)] = v[r];
+          for (int r = 0; r < 16; ++r) wb[r * (ns + ns / 32)] = v[r];
+        } else {  // ns = 16: idxD mod 32 < 16, so lpad(idxD + 16 r) = lpad(idxD) + 16 r + r/2
+#pragma unroll
+          for (int r = 0; r < 16; ++r) wb[16 * r + (r >> 1)] = v[r];
+        }
         __syncthreads();
         ns *= 16;
       }
@@ -363,7 +371,7 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
         for (int r = 0; r < R; ++r) {
           if constexpr (kAligned) {
             const int off = q * P::NT + r * (P::N / R);
-            v[q * R + r] = rbuf[pt + off + (off >> 4)];
+            v[q * R + r] = rbuf[pt + off + (off >> 5)];
           } else {
             v[q * R + r] = rbuf[lpad(t + q * P::NT + r * (P::N / R))];
           }

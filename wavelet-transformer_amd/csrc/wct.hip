@@ -128,7 +128,8 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = tid - g * P::NT;
-  const long long blk = blockIdx.x;
+  // the scale chunks of one pair share its two spectra: keep them on one XCD's L2
+  const long long blk = xcd_remap(blockIdx.x, gridDim.x);
   const long long b = blk / a.nchunks;
   const int ch = static_cast<int>(blk - b * a.nchunks);
   const int j0 = ch * a.chunk;
@@ -217,51 +218,81 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
 
 // Scale boxcar + coherence.  Row i uses rows i - K/2 .. i + (K-1)/2 (zero outside),
 // end weights 0.5; the normalisation 1/(K-1) cancels in |S12|^2 / (S1 S2) but is kept
-// so the smoothed fields match the reference.
-template <int K>
+// so the smoothed fields match the reference.  One thread = C adjacent time columns of
+// one pair (C = 2: 16-byte loads of (T1, T2) and T12 for two columns -- the pass is a
+// pure stream of the workspace); the last K rows of each column stay in registers.
+template <int C> struct ColVec;
+template <> struct ColVec<1> { using T = float2; };
+template <> struct ColVec<2> { using T = float4; };
+
+template <int K, int C>
 __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, const cpx* __restrict__ TB,
                                                    long long batch, int n0, int S, float* __restrict__ coh) {
-  const long long tiles = (n0 + 255) / 256;
+  using V = typename ColVec<C>::T;
+  constexpr int F = 2 * C;  // floats per V
+  const int ncol = n0 / C;
+  const long long tiles = (ncol + 255) / 256;
   const long long b = blockIdx.x / tiles;
-  const int tcol = static_cast<int>((blockIdx.x - b * tiles) * 256 + threadIdx.x);
-  if (tcol >= n0) return;
+  const int u = static_cast<int>((blockIdx.x - b * tiles) * 256 + threadIdx.x);
+  if (u >= ncol) return;
   constexpr int LO = K / 2;        // rows before i
   constexpr int HI = (K - 1) / 2;  // rows after i
   const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
-  const cpx* cola = TA + b * static_cast<long long>(S) * n0 + tcol;
-  const cpx* colb = TB + b * static_cast<long long>(S) * n0 + tcol;
-  float* out = coh + b * static_cast<long long>(S) * n0 + tcol;
-  float4 ring[K];
+  const V* cola = reinterpret_cast<const V*>(TA + b * static_cast<long long>(S) * n0) + u;
+  const V* colb = reinterpret_cast<const V*>(TB + b * static_cast<long long>(S) * n0) + u;
+  float* out = coh + b * static_cast<long long>(S) * n0 + static_cast<long long>(u) * C;
+  const long long ldv = n0 / C;  // row stride in V
+  float ra[K][F], rb[K][F];
 #pragma unroll
-  for (int r = 0; r < K; ++r) ring[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < K; ++r)
+#pragma unroll
+    for (int f = 0; f < F; ++f) ra[r][f] = rb[r][f] = 0.f;
   // row j enters the ring at slot j % K; output row i = j - HI is complete then.
   for (int jb = 0; jb < S + HI; jb += K) {
 #pragma unroll
     for (int r = 0; r < K; ++r) {
       const int j = jb + r;
       if (j < S) {
-        const cpx ta = cola[static_cast<long long>(j) * n0], tb = colb[static_cast<long long>(j) * n0];
-        ring[r] = make_float4(ta.x, ta.y, tb.x, tb.y);
+        const V a = cola[j * ldv], c = colb[j * ldv];
+        const float* pa = reinterpret_cast<const float*>(&a);
+        const float* pc = reinterpret_cast<const float*>(&c);
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          ra[r][f] = pa[f];
+          rb[r][f] = pc[f];
+        }
       } else {
-        ring[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int f = 0; f < F; ++f) ra[r][f] = rb[r][f] = 0.f;
       }
       const int i = j - HI;
       if (i >= 0 && i < S) {
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        float acc[2][F] = {};
 #pragma unroll
         for (int q = 0; q < K; ++q) {
           // slot of row i - LO + q  (rows i-LO .. i+HI = j-K+1 .. j)
           const int slot = (r + 1 + q) % K;
           const float wq = (K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn;
-          const int row = i - LO + q;
-          if (row >= 0) {
-            acc.x = fmaf(wq, ring[slot].x, acc.x);
-            acc.y = fmaf(wq, ring[slot].y, acc.y);
-            acc.z = fmaf(wq, ring[slot].z, acc.z);
-            acc.w = fmaf(wq, ring[slot].w, acc.w);
+          if (i - LO + q >= 0) {
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+              acc[0][f] = fmaf(wq, ra[slot][f], acc[0][f]);
+              acc[1][f] = fmaf(wq, rb[slot][f], acc[1][f]);
+            }
           }
         }
-        out[static_cast<long long>(i) * n0] = (acc.z * acc.z + acc.w * acc.w) / (acc.x * acc.y);
+        float o[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const float s1 = acc[0][2 * c], s2 = acc[0][2 * c + 1];
+          const float re = acc[1][2 * c], im = acc[1][2 * c + 1];
+          o[c] = (re * re + im * im) / (s1 * s2);
+        }
+        float* orow = out + static_cast<long long>(i) * n0;
+        if constexpr (C == 2)
+          *reinterpret_cast<float2*>(orow) = make_float2(o[0], o[1]);
+        else
+          orow[0] = o[0];
       }
     }
   }
@@ -302,11 +333,17 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, hipStream_t s
 template <int K>
 static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0, int S, float* coh,
                           hipStream_t st) {
-  const long long tiles = (n0 + 255) / 256;
+  const bool pairs = (n0 % 2) == 0;  // 16-byte column pairs need even rows
+  const long long ncol = pairs ? n0 / 2 : n0;
+  const long long tiles = (ncol + 255) / 256;
   const long long grid = batch * tiles;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  hipLaunchKernelGGL(wct_phase_b<K>, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB, batch, n0,
-                     S, coh);
+  if (pairs)
+    hipLaunchKernelGGL((wct_phase_b<K, 2>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
+                       batch, n0, S, coh);
+  else
+    hipLaunchKernelGGL((wct_phase_b<K, 1>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
+                       batch, n0, S, coh);
   return launch_status();
 }
 

@@ -1,0 +1,147 @@
+// Monte-Carlo coherence significance pieces: pycwt's
+// wct_significance, reached from src/wct.py:106-118 when run_wct is called with
+// calculate_signficance=True.  Per Monte-Carlo pass pycwt draws two AR(1) red-noise
+// series (helpers.rednoise), runs the coherence of the pair and counts
+// floor(R2 * nbins) per scale over the points outside the cone of influence.
+//
+// Here the passes are batched: K10 draws all 2 x mc_count series at once, the
+// coherence kernels (wct.hip) run on the batch as on any pair batch, and K11 folds
+// the coherence planes into the [scale][bin] counter.  The quantile step (a few
+// thousand numbers) stays on the host.
+#include "common.hpp"
+
+namespace wtmi {
+
+// Philox4x32-10 (Salmon et al., SC'11), counter-based: stream (series, block) -> 4 words.
+struct Philox {
+  static constexpr unsigned M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  static constexpr unsigned W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+  __device__ static uint4 gen(uint4 c, uint2 k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const unsigned long long p0 = static_cast<unsigned long long>(M0) * c.x;
+      const unsigned long long p1 = static_cast<unsigned long long>(M1) * c.z;
+      const unsigned hi0 = static_cast<unsigned>(p0 >> 32), lo0 = static_cast<unsigned>(p0);
+      const unsigned hi1 = static_cast<unsigned>(p1 >> 32), lo1 = static_cast<unsigned>(p1);
+      c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+      k.x += W0;
+      k.y += W1;
+    }
+    return c;
+  }
+};
+
+__device__ __forceinline__ double u01(unsigned a, unsigned b) {  // (0, 1), 53 bits
+  const unsigned long long v = (static_cast<unsigned long long>(a) << 21) ^ (b >> 11);
+  return (static_cast<double>(v & ((1ull << 53) - 1)) + 0.5) * 0x1.0p-53;
+}
+
+// K10: AR(1) red noise, pycwt helpers.rednoise(N, g, a=1):
+//   y = lfilter([1, 0], [1, -g], randn(N + tau))[tau:], tau = ceil(-2 / ln|g|).
+// One thread per series (the recurrence is sequential; N <= 16384 keeps this in the
+// tens of microseconds).  Normals from Box-Muller on Philox words, fp64 recurrence.
+__global__ void __launch_bounds__(64) rednoise_kernel(float* __restrict__ out, long long ld,
+                                                      long long count, int n, double g, int tau,
+                                                      unsigned long long seed,
+                                                      unsigned long long first) {
+  const long long c = blockIdx.x * 64ll + threadIdx.x;
+  if (c >= count) return;
+  const unsigned long long sid = first + static_cast<unsigned long long>(c);
+  const uint2 key = make_uint2(static_cast<unsigned>(seed), static_cast<unsigned>(seed >> 32));
+  float* row = out + c * ld;
+  double y = 0.0;
+  const int total = n + tau;
+  for (int i0 = 0; i0 < total; i0 += 2) {
+    // one Philox block -> two normals
+    const uint4 w = Philox::gen(make_uint4(static_cast<unsigned>(i0 >> 1), static_cast<unsigned>(sid),
+                                           static_cast<unsigned>(sid >> 32), 0x5eed5u), key);
+    const double r = sqrt(-2.0 * log(u01(w.x, w.y)));
+    double s, co;
+    sincospi(2.0 * u01(w.z, w.w), &s, &co);
+    const double e[2] = {r * co, r * s};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = i0 + q;
+      if (i < total) {
+        y = fma(g, y, e[q]);
+        if (i >= tau) row[i - tau] = static_cast<float>(y);
+      }
+    }
+  }
+}
+
+// K11: per-scale coherence counter.  Block (s, part) walks the pairs
+// part, part + parts, ... of scale s (s < n_hist_scales) over t in [t_lo[s], t_hi[s])
+// -- the points outside the COI, an interval because the COI is a triangle -- and
+// counts floor(R2 * nbins) (clamped to [0, nbins - 1]; NaN skipped) into an LDS
+// histogram, then adds the non-zero bins to hist[s][:].
+constexpr int kHistThreads = 256;
+constexpr int kMaxBins = 4096;
+
+__global__ void __launch_bounds__(kHistThreads) coherence_hist_kernel(
+    const float* __restrict__ coh, long long batch, long long n0, int S, const int* __restrict__ t_lo,
+    const int* __restrict__ t_hi, int nbins, int parts, unsigned* __restrict__ hist) {
+  __shared__ unsigned h[kMaxBins];
+  const int s = blockIdx.x / parts;
+  const int part = blockIdx.x - s * parts;
+  for (int i = threadIdx.x; i < nbins; i += kHistThreads) h[i] = 0u;
+  __syncthreads();
+  const long long lo = t_lo[s], hi = t_hi[s];
+  const float fb = static_cast<float>(nbins);
+  for (long long p = part; p < batch; p += parts) {
+    const float* row = coh + (p * S + s) * n0;
+    for (long long t = lo + threadIdx.x; t < hi; t += kHistThreads) {
+      const float r = row[t];
+      if (!(r == r)) continue;
+      int bin = static_cast<int>(floorf(r * fb));
+      bin = bin < 0 ? 0 : (bin >= nbins ? nbins - 1 : bin);
+      atomicAdd(&h[bin], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nbins; i += kHistThreads)
+    if (h[i]) atomicAdd(&hist[static_cast<long long>(s) * nbins + i], h[i]);
+}
+
+}  // namespace wtmi
+
+using namespace wtmi;
+
+extern "C" int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g,
+                             unsigned long long seed, unsigned long long first_series, void* stream) {
+  if (!out || count < 0 || n < 0 || ld < n || !(g > -1.0 && g < 1.0)) return kErrArg;
+  if (n > (1ll << 30)) return kErrUnsupported;
+  if (count == 0 || n == 0) return kOk;
+  int tau = 0;
+  if (g != 0.0) {
+    const double tt = ceil(-2.0 / log(fabs(g)));
+    if (tt > (1 << 26)) return kErrUnsupported;
+    tau = static_cast<int>(tt);
+  }
+  const long long blocks = (count + 63) / 64;
+  if (blocks > 0x7fffffffll) return kErrUnsupported;
+  hipLaunchKernelGGL(rednoise_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), out, ld, count, static_cast<int>(n), g, tau, seed,
+                     first_series);
+  return launch_status();
+}
+
+extern "C" int wtmi_coherence_histogram(const float* coh, long long batch, long long n0, int n_scales,
+                                        const int* t_lo, const int* t_hi, int n_hist_scales, int nbins,
+                                        unsigned* hist, void* stream) {
+  if (!coh || !t_lo || !t_hi || !hist || batch < 0 || n0 < 0 || n_scales < 0 || n_hist_scales < 0 ||
+      n_hist_scales > n_scales || nbins < 1)
+    return kErrArg;
+  if (nbins > kMaxBins) return kErrUnsupported;
+  if (batch == 0 || n0 == 0 || n_hist_scales == 0) return kOk;
+  // enough blocks to fill the chip: split each scale's pairs into parts
+  long long parts = (2048 + n_hist_scales - 1) / n_hist_scales;
+  if (parts > batch) parts = batch;
+  if (parts < 1) parts = 1;
+  const long long grid = parts * n_hist_scales;
+  if (grid > 0x7fffffffll) return kErrUnsupported;
+  hipLaunchKernelGGL(coherence_hist_kernel, dim3(static_cast<unsigned>(grid)), dim3(kHistThreads), 0,
+                     static_cast<hipStream_t>(stream), coh, batch, n0, n_scales, t_lo, t_hi, nbins,
+                     static_cast<int>(parts), hist);
+  return launch_status();
+}

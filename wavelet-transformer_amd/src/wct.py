@@ -4,9 +4,9 @@
 ``calculate_signficance`` (src/wct.py:96-140).  Coherence and phase arrows come from
 the fused coherence kernels (``wtmi_wct_morlet``).  With significance off the
 reference divides by ``signif = [0]`` and returns an all-inf ratio (quirk B.8);
-that is reproduced.  Significance ON needs pycwt's Monte-Carlo
-``wct_significance`` -- SURVEY 8(f) row 1, not built yet: it raises
-NotImplementedError.
+that is reproduced.  Significance ON runs pycwt's Monte-Carlo ``wct_significance``
+on the GPU (``transforms.wct_significance``: red noise K10, batched coherence,
+counter K11; 300 passes, in-process cache like pycwt's ``cache=True``).
 """
 
 from __future__ import annotations
@@ -81,10 +81,6 @@ def run_wct(wavelet_coherence_transform: Type[DataForWCT], calculate_signficance
     y1, y2 = np.asarray(d.y1_values), np.asarray(d.y2_values)
     if y1.size != y2.size:
         raise AssertionError("Input signals must have the same size")
-    if calculate_signficance:
-        raise NotImplementedError(
-            "run_wct(calculate_signficance=True) needs the Monte-Carlo wct_significance "
-            "(SURVEY 8(f) row 1), not implemented yet")
     d1 = transforms._to_dev(y1).reshape(1, -1)
     d2 = transforms._to_dev(y2).reshape(1, -1)
     x1 = ops.affine(d1, transforms.normalize_coefs(ops.series_moments(d1)), torch.float32)
@@ -93,7 +89,17 @@ def run_wct(wavelet_coherence_transform: Type[DataForWCT], calculate_signficance
                                           normalize=False, want_uv=True)
     n0 = y1.size
     coherence = transforms._np(res["coh"][0], np.float64)
-    signif = np.asarray([0])
+    if calculate_signficance:
+        # pycwt.wct(sig=True): AR(1) of the raw series, then the Monte-Carlo levels at
+        # the transform's own resolution (J = -1 -> round(log2(n dt / s0) / dj))
+        J = int(np.round(np.log2(n0 * d.delta_t / d.initial_scale) / d.delta_j))
+        a1, _, _ = transforms.ar1(y1)
+        a2, _, _ = transforms.ar1(y2)
+        signif = transforms.wct_significance(a1, a2, d.delta_t, d.delta_j, d.initial_scale, J,
+                                             significance_level=significance_level,
+                                             wavelet=mother, cache=True)
+    else:
+        signif = np.asarray([0])
     with np.errstate(divide="ignore", invalid="ignore"):
         sig95 = np.abs(coherence) / (np.ones([1, n0]) * signif[:, None])
     coi = transforms.cone_of_influence(n0, d.delta_t, mother)

@@ -207,6 +207,43 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     return res
 
 
+def rednoise(count: int, n: int, g: float, seed: int, *, first_series: int = 0,
+             device=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[count, n] float32 AR(1) red noise (pycwt helpers.rednoise(n, g, 1) per row),
+    drawn on the GPU from Philox4x32-10 stream (seed, first_series + row)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if out is None:
+        out = torch.empty((count, n), dtype=torch.float32, device=dev)
+    _check_dev(out)
+    with torch.cuda.device(out.device):
+        _lib.call("wtmi_rednoise", _ptr(out), out.stride(0), count, n, float(g),
+                  C.c_ulonglong(int(seed) & ((1 << 64) - 1)), C.c_ulonglong(int(first_series)),
+                  _stream(out.device))
+    return out
+
+
+def coherence_histogram(coh: torch.Tensor, t_lo: torch.Tensor, t_hi: torch.Tensor,
+                        n_hist_scales: int, nbins: int = 1000,
+                        hist: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Accumulate floor(coh * nbins) counts of coh [B, S, n0] over t in [t_lo[s], t_hi[s])
+    for s < n_hist_scales into hist [n_hist_scales, nbins] (int32 view of uint32)."""
+    if coh.dim() == 2:
+        coh = coh.unsqueeze(0)
+    coh = coh.to(torch.float32).contiguous()
+    dev = _check_dev(coh)
+    B, S, n0 = coh.shape
+    lo = t_lo.to(device=dev, dtype=torch.int32).contiguous()
+    hi = t_hi.to(device=dev, dtype=torch.int32).contiguous()
+    if lo.numel() < n_hist_scales or hi.numel() < n_hist_scales:
+        raise ValueError("t_lo / t_hi need one entry per histogram scale")
+    if hist is None:
+        hist = torch.zeros((n_hist_scales, nbins), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_coherence_histogram", _ptr(coh), B, n0, S, _ptr(lo), _ptr(hi),
+                  int(n_hist_scales), int(nbins), _ptr(hist), _stream(dev))
+    return hist
+
+
 # -------------------------------------------------------------------------- MODWT
 def _taps(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.float64))

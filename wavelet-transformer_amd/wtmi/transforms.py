@@ -260,23 +260,122 @@ def wct_batch(y1: torch.Tensor, y2: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wa
 
 def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
         wavelet="morlet", normalize=True, **kwargs):
-    """pycwt-compatible ``wct``: (WCT, aWCT, coi, freq, sig); ``**kwargs`` are swallowed
-    as in pycwt (``cache=``, and ``delta_j=`` -- reference quirk B.5)."""
+    """pycwt-compatible ``wct``: (WCT, aWCT, coi, freq, sig).  ``**kwargs`` reach
+    ``wct_significance`` when ``sig`` (``cache=``, ``mc_count=``, ``seed=``) and are
+    otherwise swallowed as in pycwt (``delta_j=`` -- reference quirk B.5)."""
     wavelet = as_morlet(wavelet)
     if np.asarray(y1).size != np.asarray(y2).size:
         raise AssertionError("Input signals must have the same size")
-    if sig:
-        raise NotImplementedError(
-            "wct(sig=True): the Monte-Carlo wct_significance is SURVEY 8(f) row 1 and not "
-            "implemented yet; call with sig=False")
     d1, d2 = _to_dev(y1).reshape(1, -1), _to_dev(y2).reshape(1, -1)
     x1 = _norm32(d1) if normalize else d1.to(torch.float32)
     x2 = _norm32(d2) if normalize else d2.to(torch.float32)
     res, sj, freq = wct_batch(x1, x2, dt, dj, s0, J, wavelet, normalize=False, want_uv=False,
                               want_phase=True)
     n0 = d1.shape[1]
+    if sig:
+        if s0 == -1:
+            s0 = 2 * dt / wavelet.flambda()
+        if J == -1:
+            J = int(np.round(np.log2(n0 * dt / s0) / dj))
+        a1, _, _ = ar1(y1)
+        a2, _, _ = ar1(y2)
+        kw = {k: v for k, v in kwargs.items() if k in ("cache", "mc_count", "seed", "progress")}
+        sig = wct_significance(a1, a2, dt=dt, dj=dj, s0=s0, J=J,
+                               significance_level=significance_level, wavelet=wavelet, **kw)
+    else:
+        sig = np.asarray([0])
     return (_np(res["coh"][0], np.float64), _np(res["phase"][0], np.float64),
-            cone_of_influence(n0, dt, wavelet), freq, np.asarray([0]))
+            cone_of_influence(n0, dt, wavelet), freq, sig)
+
+
+# ------------------------------------------------------ WCT Monte-Carlo significance
+def wct_sig_geometry(dt, dj, s0, J, wavelet="morlet"):
+    """pycwt wct_significance set-up: noise length N = ceil(6 s0 2^(J dj) / dt), scales,
+    and per scale the interval [t_lo, t_hi) of points outside the cone of influence
+    (period_s <= coi_t; the COI is a triangle, so the set is an interval);
+    maxscale = last scale with any such point (the counter runs over s < maxscale)."""
+    wavelet = as_morlet(wavelet)
+    ms = s0 * (2 ** (J * dj)) / dt
+    N = int(np.ceil(ms * 6))
+    sj = s0 * 2 ** (np.arange(0, J + 1) * dj)
+    period = wavelet.flambda() * sj
+    coi = cone_of_influence(N, dt, wavelet)
+    t_lo = np.zeros(J + 1, dtype=np.int32)
+    t_hi = np.zeros(J + 1, dtype=np.int32)
+    anyout = np.zeros(J + 1, dtype=bool)
+    for s in range(J + 1):
+        idx = np.nonzero(period[s] <= coi)[0]
+        if idx.size:
+            t_lo[s], t_hi[s] = idx[0], idx[-1] + 1
+            anyout[s] = True
+    if not anyout.any():
+        raise ValueError("no scale has points outside the cone of influence")
+    maxscale = int(np.nonzero(anyout)[0][-1])
+    return N, sj, t_lo, t_hi, anyout, maxscale
+
+
+def significance_from_histogram(wlc: np.ndarray, anyout: np.ndarray, maxscale: int,
+                                significance_level: float = 0.95) -> np.ndarray:
+    """Per-scale coherence level at ``significance_level`` from the Monte-Carlo counters,
+    as pycwt: NaN where a scale has points outside the COI, then for s < maxscale the
+    quantile interpolated over the non-empty bins (P = (cumsum - 0.5) / total) on the
+    mid-bin grid (b + 0.5) / nbins."""
+    nbins = wlc.shape[1]
+    sig95 = np.zeros(anyout.size)
+    sig95[anyout] = np.nan
+    r2y = (np.arange(nbins) + 0.5) / nbins
+    for s in range(maxscale):
+        sel = wlc[s] != 0
+        if not sel.any():
+            continue
+        P = np.cumsum(wlc[s, sel])
+        P = (P - 0.5) / P[-1]
+        sig95[s] = np.interp(significance_level, P, r2y[sel])
+    return sig95
+
+
+_sig_cache: dict = {}
+
+
+def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="morlet",
+                     mc_count=300, progress=True, cache=True, seed=None, nbins=1000,
+                     max_pairs_per_launch=128):
+    """pycwt ``wct_significance`` on the GPU: mc_count passes of two AR(1) red-noise
+    series (al1, al2), their coherence, and the per-scale counter of floor(R2 * nbins)
+    outside the COI, batched max_pairs_per_launch passes per launch.  ``cache`` keeps
+    results in process memory keyed on every argument (pycwt keeps a disk cache);
+    ``seed`` None draws a fresh one, as pycwt's unseeded draws do."""
+    wavelet = as_morlet(wavelet)
+    key = (float(al1), float(al2), float(dt), float(dj), float(s0), int(J),
+           float(significance_level), wavelet.f0, int(mc_count), nbins, seed)
+    if cache and key in _sig_cache:
+        return _sig_cache[key].copy()
+    N, sj, t_lo, t_hi, anyout, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
+    if seed is None:
+        seed = int(np.random.SeedSequence().entropy) & ((1 << 64) - 1)
+    dev = device()
+    lo = torch.as_tensor(t_lo, device=dev)
+    hi = torch.as_tensor(t_hi, device=dev)
+    hist = torch.zeros((max(maxscale, 1), nbins), dtype=torch.int32, device=dev)
+    K = boxcar_rows(wavelet, dj)
+    ws = None
+    for p0 in range(0, int(mc_count), max_pairs_per_launch):
+        B = min(max_pairs_per_launch, int(mc_count) - p0)
+        n1 = ops.rednoise(B, N, al1, seed, first_series=p0, device=dev)
+        n2 = ops.rednoise(B, N, al2, seed, first_series=int(mc_count) + p0, device=dev)
+        need = ops.wct_workspace_bytes(B, N, sj.size)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        coh = ops.wct_morlet(n1, n2, sj, dt, wavelet.f0, boxcar=K, want_uv=False, workspace=ws)["coh"]
+        if maxscale > 0:
+            ops.coherence_histogram(coh, lo, hi, maxscale, nbins, hist=hist)
+    wlc = _np(hist).view(np.uint32).astype(np.float64)
+    full = np.zeros((sj.size, nbins))
+    full[:wlc.shape[0]] = wlc[:maxscale] if maxscale > 0 else 0
+    sig95 = significance_from_histogram(full, anyout, maxscale, significance_level)
+    if cache:
+        _sig_cache[key] = sig95.copy()
+    return sig95
 
 
 def _norm32(d: torch.Tensor) -> torch.Tensor:
