@@ -1,0 +1,46 @@
+#!/bin/bash
+# One GPU session producing the judged artifacts of a round (run via gpurun):
+#   1. PMC FETCH_SIZE / WRITE_SIZE passes per config -> gpurun_out/pmc_traffic.json
+#      (copied into profiles/$ROUND/ on the box so the bench lines carry "traffic")
+#   2. rocprofv3 --kernel-trace --stats per config   -> gpurun_out/prof_<cfg>/
+#   3. bench.py per config (CPU baseline included)   -> gpurun_out/bench_<cfg>.json
+# Every GPU step has its own time limit; a crash / abort / timeout ends the session.
+set -u
+ROUND=${ROUND:-r01}
+CFGS=${CFGS:-"c2 c3 c4 c5"}
+OUT=gpurun_out
+mkdir -p $OUT profiles/$ROUND
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; echo "FATAL in $name"; exit $rc; fi
+}
+if [ "${SKIP_PMC:-0}" != 1 ]; then
+  for c in $CFGS; do
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      run pmc_${c}_$ctr 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/pmc_${c}_$ctr -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
+    done
+    python scripts/pmc_traffic.py $c $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/pmc_traffic.json > /dev/null || exit 1
+  done
+  cp $OUT/pmc_traffic.json profiles/$ROUND/pmc_traffic.json
+fi
+if [ "${SKIP_PROF:-0}" != 1 ]; then
+  for c in $CFGS; do
+    STEPS_K=10
+    [ $c = c2 ] && STEPS_K=50
+    run prof_$c 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$c -o run -- python bench.py --config $c --steps $STEPS_K --warmup 5 --no-cpu-baseline
+    python scripts/trace_mean.py $OUT/prof_$c $STEPS_K > $OUT/prof_$c/timed_mean.txt
+  done
+fi
+for c in $CFGS; do
+  ARGS=""
+  [ $c = c2 ] || ARGS="--steps 10 --warmup 3"
+  run bench_$c 600 python bench.py --config $c $ARGS
+  grep '^{' $OUT/bench_$c.log | tail -1 > $OUT/bench_$c.json
+  cut -c1-200 $OUT/bench_$c.json
+done
+echo ALLDONE

@@ -183,3 +183,19 @@ def test_wavedec_batched_vs_oracle():
     for b in (0, 17, 31):
         ref = np.concatenate(ds.wavedec(x[b].astype(np.float64), w.dec_lo, w.dec_hi, lev))
         assert np.abs(ct[b] - ref).max() <= TOL * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("n,J", [(16384, 10), (8192, 12), (4096, 3)])
+def test_imodwt_adjoint_and_masks_at_bench_shape(n, J, db4):
+    """Synthesis on NON-range input (adjoint, every tap exercised) and with row masks at
+    the C3 shape (the dilation-chain kernel's levels j >= 3) vs the textbook oracle."""
+    rng = np.random.default_rng(n + J)
+    w = rng.standard_normal((2, J + 1, n)).astype(np.float32)
+    ops = _ops()
+    wd = torch.tensor(w, device="cuda")
+    for keep in ((1 << (J + 1)) - 1, 0b101 << (J - 2), 1 << J):
+        got = ops.imodwt(wd, db4["dec_lo"], db4["dec_hi"], keep).cpu().numpy()
+        for b in range(2):
+            wm = w[b].astype(np.float64) * np.array([(keep >> r) & 1 for r in range(J + 1)])[:, None]
+            ref = ms.imodwt_direct(wm, db4["dec_lo"], db4["dec_hi"])
+            assert np.abs(got[b] - ref).max() <= 3 * TOL * np.abs(ref).max(), (keep, b)
