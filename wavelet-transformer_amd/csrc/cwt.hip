@@ -236,7 +236,10 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   // Scale chunking: enough workgroups to fill 256 CUs several times, while keeping
   // at least 4 row-iterations per workgroup to amortise the forward FFT.
   const int rows = G::ROWS;
-  const int target = env_int("WTMI_CWT_TARGET_WG", 4096);
+  // Few, long workgroups: each one's start-up (twiddles, forward FFT) amortises over
+  // more scales.  Measured (ms): C2 (LOGN 12, 3 WG/CU) 1024 WG 0.871, 2048 0.839,
+  // 4096 0.860; C5 chunk (LOGN 13, 2 WG/CU) 512 30.9, 1024 30.86, 2048 31.2, 4096 32.9.
+  const int target = env_int("WTMI_CWT_TARGET_WG", LOGN >= 13 ? 1024 : 2048);
   long long want = (target + a.batch - 1) / a.batch;
   const int max_chunks = (a.S + 4 * rows - 1) / (4 * rows);
   int nch = static_cast<int>(want < 1 ? 1 : want);

@@ -163,23 +163,25 @@ __host__ __device__ constexpr int twl_base(int p) { return p <= 1 ? 0 : 16; }
 
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 5); }
 
-// exp(+2 pi i num / den), correctly rounded from double.
-__device__ __forceinline__ cpx expi_frac(long long num, long long den) {
-  num %= den;
-  double s, c;
-  sincospi(2.0 * static_cast<double>(num) / static_cast<double>(den), &s, &c);
-  return mkc(static_cast<float>(c), static_cast<float>(s));
+// exp(+2 pi i num / den) for a power-of-two den <= 2^14: 2 num / den is exact in
+// float, and sincospif is accurate to ~1 ulp -- the double-precision form cost a
+// measurable share of each workgroup's start-up (8-16 fp64 sincospi per thread).
+__device__ __forceinline__ cpx expi_frac(int num, int den) {
+  num &= den - 1;
+  float s, c;
+  sincospif(2.f * static_cast<float>(num) / static_cast<float>(den), &s, &c);
+  return mkc(c, s);
 }
 
 // Per-thread base twiddles (inverse sign; the forward transform conjugates them).
 template <int LOGN>
 __device__ __forceinline__ void fft_twiddles(cpx* tw, int t) {
   using P = FftPlan<LOGN>;
-  long long ns = 16;
+  int ns = 16;
 #pragma unroll
   for (int p = 1; p < P::P16; ++p) {
-    const long long k = t & (ns - 1);
-    const long long M = ns * 16;
+    const int k = t & (ns - 1);
+    const int M = ns * 16;
     tw[4 * (p - 1) + 0] = expi_frac(k, M);
     tw[4 * (p - 1) + 1] = expi_frac(2 * k, M);
     tw[4 * (p - 1) + 2] = expi_frac(4 * k, M);
@@ -189,7 +191,7 @@ __device__ __forceinline__ void fft_twiddles(cpx* tw, int t) {
   if constexpr (P::REM > 1) {
     constexpr int base = 4 * (P::P16 - 1);
 #pragma unroll
-    for (int e = 0; e < P::NTW_REM; ++e) tw[base + e] = expi_frac(static_cast<long long>(t) << e, P::N);
+    for (int e = 0; e < P::NTW_REM; ++e) tw[base + e] = expi_frac(t << e, P::N);
   }
 }
 
@@ -199,7 +201,7 @@ __device__ __forceinline__ void fft_twiddles_tail(cpx* tw, int t) {
   using P = FftPlan<LOGN>;
   if constexpr (P::REM > 1) {
 #pragma unroll
-    for (int e = 0; e < P::NTW_REM; ++e) tw[e] = expi_frac(static_cast<long long>(t) << e, P::N);
+    for (int e = 0; e < P::NTW_REM; ++e) tw[e] = expi_frac(t << e, P::N);
   }
 }
 
@@ -208,8 +210,8 @@ template <int LOGN>
 __device__ __forceinline__ void fft_twiddle_table(float4* tab, int tid, int nthreads) {
   using P = FftPlan<LOGN>;
   for (int i = tid; i < P::TWL_E; i += nthreads) {
-    const long long M = i < 16 ? 256 : 4096;  // pass 1: 16 * 16, pass 2: 256 * 16
-    const long long k = i < 16 ? i : i - 16;
+    const int M = i < 16 ? 256 : 4096;  // pass 1: 16 * 16, pass 2: 256 * 16
+    const int k = i < 16 ? i : i - 16;
     const cpx w1 = expi_frac(k, M), w2 = expi_frac(2 * k, M);
     const cpx w4 = expi_frac(4 * k, M), w8 = expi_frac(8 * k, M);
     tab[i] = make_float4(w1.x, w1.y, w2.x, w2.y);

@@ -365,10 +365,44 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
   }
 }
 
+// Synthesis level along dilation chains (levels with a dilation of dq >= 1 float4
+// groups).  Thread (c, r) owns the M groups q = c*M*dq + m*dq + r (m = 0..M-1): output
+// m needs taps m .. m+L-1 of the same chain, so the thread loads M+L-1 taps of W_j
+// (global) and of V_j (LDS) once and slides over them -- (M+L-1)/M loads per output
+// instead of L (the 8x re-read of W_j through L2 is what bounds the stride-T form).
+// Lanes with consecutive r read consecutive groups: coalesced for dq >= 64 groups,
+// dq-group contiguous runs below that.  Needs ng == M*T and ng % (M*dq) == 0.
+template <int L, int M>
+__device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, const float4* __restrict__ W4,
+                                               int ng, int dqlog, const float (&hs)[L],
+                                               const FilterBank& fb, int tid, float4 (&vreg)[M]) {
+  const int dq = 1 << dqlog;
+  const int q0 = (tid >> dqlog) * M * dq + (tid & (dq - 1));
+  float4 wv[M + L - 1], vv[M + L - 1];
+#pragma unroll
+  for (int k = 0; k < M + L - 1; ++k) wv[k] = W4[(q0 + k * dq) % ng];  // taps may wrap >1x
+#pragma unroll
+  for (int k = 0; k < M + L - 1; ++k) vv[k] = V4[(q0 + k * dq) % ng];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      fma4(acc, fb.g[l], vv[m + l]);
+      fma4(acc, hs[l], wv[m + l]);
+    }
+    vreg[m] = acc;
+    pin4(vreg[m]);
+  }
+  return q0;
+}
+
 // MODE 0: W_j copied global -> LDS at the start of each level.
 // MODE 1: as 0, but W_{j-1} is prefetched into registers while level j computes.
 // MODE 2: W_j taps read straight from global memory (L1/L2); LDS holds V only (n floats),
 //         so two workgroups fit per CU and one's loads overlap the other's math.
+// MODE 3: as 2, but levels with a whole-group dilation run along dilation chains
+//         (syn_level_chain: each W_j / V_j tap loaded ~2x instead of 8x).
 template <int L, int GROUPS, int T, int MODE>
 __global__ void __launch_bounds__(T)
     imodwt_vec_kernel(const float* __restrict__ w, int n, int level, FilterBank fb, unsigned long long keep,
@@ -411,7 +445,22 @@ __global__ void __launch_bounds__(T)
     int tl = tid;
     asm volatile("" : "+v"(tl));  // per-level copy: keeps address math out of LICM
     float4 vreg[GROUPS];
-    syn_level<L, GROUPS, T>(V4, MODE == 2 ? wr : W4, ng, dm, wsel, fb, tl, vreg);
+    int dqlog = -1;
+    if (MODE == 3 && (dm & 3) == 0 && GROUPS * T == ng) {
+      const int dq = dm >> 2;
+      if ((dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) dqlog = __builtin_ctz(dq);
+    }
+    if (dqlog >= 0) {
+      float hs[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) hs[l] = wsel * fb.h[l];
+      const int q0 = syn_level_chain<L, GROUPS>(V4, wr, ng, dqlog, hs, fb, tl, vreg);
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) V4[q0 + (k << dqlog)] = vreg[k];
+      continue;
+    }
+    syn_level<L, GROUPS, T>(V4, MODE >= 2 ? wr : W4, ng, dm, wsel, fb, tl, vreg);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < GROUPS; ++k) {
@@ -529,15 +578,17 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
     else if (ng <= 1024)
       launch(imodwt_vec_kernel<8, 1, 1024, 0>, 1024);
     else if (ng <= 2048)
-      launch(imodwt_vec_kernel<8, 2, 1024, 0>, 1024);
+      launch_lds(imodwt_vec_kernel<8, 2, 1024, 3>, 1024, lds / 2);
     else if (var == 1)
       launch(imodwt_vec_kernel<8, 4, 1024, 1>, 1024);
     else if (var == 2)
       launch_lds(imodwt_vec_kernel<8, 4, 1024, 2>, 1024, lds / 2);
     else if (var == 3)
       launch(imodwt_vec_kernel<8, 4, 1024, 0>, 1024);
-    else  // C3 A/B (ms): W from global, 2 WG/CU 2.00; W via LDS 2.11; + register prefetch 2.71
+    else if (var == 4)  // C3 A/B (ms): W from global, 2 WG/CU 2.00; W via LDS 2.11; + register prefetch 2.71
       launch_lds(imodwt_vec_kernel<8, 8, 512, 2>, 512, lds / 2);
+    else
+      launch_lds(imodwt_vec_kernel<8, 8, 512, 3>, 512, lds / 2);
   } else if (n_taps == 8) {
     allow_lds(imodwt_kernel<8>, lds);
     hipLaunchKernelGGL(imodwt_kernel<8>, dim3(batch), dim3(block), lds, st, w, ni, level, n_taps, fb,

@@ -311,7 +311,11 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, hipStream_t s
     if (rc != kOk) return rc;
   }
   const int rows = G::ROWS;
-  long long want = (4096 + a.batch - 1) / a.batch;
+  const char* ev = getenv("WTMI_WCT_TARGET_WG");
+  // phase A rows are 6 FFTs each: more, shorter workgroups balance better here
+  // (C4 ms: 1024 WG 6.27, 2048 6.19, 4096 6.16, 8192 6.02)
+  const long long target = ev ? atoll(ev) : 8192;
+  long long want = (target + a.batch - 1) / a.batch;
   const int max_chunks = (a.S + 4 * rows - 1) / (4 * rows);
   int nch = static_cast<int>(want < 1 ? 1 : want);
   if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
