@@ -38,8 +38,10 @@ __device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, 
       rv = uniform_rsrc(pv_);
     }
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
+    for (int m = 0; m < 16; ++m)
       if constexpr (KIND & kOutW) buf_st(v[m], rw, 8 * t, 8 * m * P::NT);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
       const float pw = cabs2(v[m]);
       if constexpr (KIND & kOutPow) buf_st(pw, rp, 4 * t, 4 * m * P::NT);
       if constexpr (KIND & kOutSig) buf_st(pw * sg, rs, 4 * t, 4 * m * P::NT);

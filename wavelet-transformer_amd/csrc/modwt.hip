@@ -264,7 +264,11 @@ __device__ __forceinline__ void fma4(float4& acc, float c, const float4& s) {
 // result before the barrier; without both, the compiler hoists per-group address math
 // out of the level loop and sinks the tap FMAs past the barrier, keeping every LDS
 // operand live (256 VGPRs + spills).
-template <int L, int GROUPS, int T>
+// CHAIN: levels with a whole-group dilation use the dilation-chain mapping of
+// syn_level_chain (taps m-L+1 .. m of the thread's chain, M+L-1 LDS reads for M
+// outputs instead of L*M); W_j stores then run along the chain (coalesced for
+// dq >= 64 groups, dq-group runs below).
+template <int L, int GROUPS, int T, bool CHAIN = false>
 __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ x, long long ld,
                                                       int n, int level, FilterBank fb,
                                                       float* __restrict__ w) {
@@ -282,6 +286,34 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
     int tl = tid;
     asm volatile("" : "+v"(tl));
     float4 vreg[GROUPS];
+    if (CHAIN && (dm & 3) == 0 && GROUPS * T == ng) {
+      const int dq = dm >> 2;
+      if ((dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) {
+        const int dqlog = __builtin_ctz(dq);
+        const int q0 = (tl >> dqlog) * GROUPS * dq + (tl & (dq - 1));
+        float4 vv[GROUPS + L - 1];  // chain elements q0 + (k - L + 1) dq
+#pragma unroll
+        for (int k = 0; k < GROUPS + L - 1; ++k)
+          vv[k] = V4[(q0 + (k - (L - 1)) * dq + (L - 1) * ng) % ng];
+#pragma unroll
+        for (int m = 0; m < GROUPS; ++m) {
+          float4 aw = make_float4(0.f, 0.f, 0.f, 0.f), av = aw;
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            fma4(aw, fb.h[l], vv[m + L - 1 - l]);
+            fma4(av, fb.g[l], vv[m + L - 1 - l]);
+          }
+          wrow[q0 + m * dq] = aw;
+          vreg[m] = av;
+          pin4(vreg[m]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < GROUPS; ++m) V4[q0 + m * dq] = vreg[m];
+        __syncthreads();
+        continue;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < GROUPS; ++k) {
       const int q = min(tl + k * T, ng - 1);
@@ -534,6 +566,8 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
       launch(modwt_vec_kernel<8, 2, 1024>, 1024);
     else if (var == 1)
       launch(modwt_vec_kernel<8, 4, 1024>, 1024);
+    else if (var == 2)
+      launch(modwt_vec_kernel<8, 8, 512, true>, 512);
     else
       launch(modwt_vec_kernel<8, 8, 512>, 512);  // C3 A/B: 1.62 vs 1.65 ms
   } else if (n_taps == 8) {
