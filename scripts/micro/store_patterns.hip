@@ -1,0 +1,144 @@
+// Store-pattern microbenchmark (diagnostic only): how fast can a grid of workgroups write
+// 4.3 GB of complex64 rows (32 KB each) under the CWT kernel's row-ownership pattern vs a
+// linear sweep, with 8-byte and 16-byte stores per lane.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int ROWB = 32768;             // bytes per row (4096 complex64)
+constexpr long long NROWS = 131072;     // 1024 series x 128 scales
+
+// mode 0: WG owns ROWS_PER_WG consecutive rows (CWT C2 mapping), rows walked in order
+// mode 1: WG w handles rows w + i * nwg (concurrent WGs write consecutive rows)
+template <int VEC, int NT = 0>
+__global__ void __launch_bounds__(256) rows_kernel(char* out, int mode, int nwg, int rows_per_wg) {
+  const int t = threadIdx.x;
+  for (int i = 0; i < rows_per_wg; ++i) {
+    long long row = mode == 0 ? (long long)blockIdx.x * rows_per_wg + i : (long long)i * nwg + blockIdx.x;
+    if (row >= NROWS) return;
+    char* base = out + row * ROWB;
+    if (VEC == 2) {
+      f2* p = reinterpret_cast<f2*>(base);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (NT == 1) __builtin_nontemporal_store(f2{(float)i, (float)m}, p + t + m * 256);
+        else if (NT == 2) {
+          __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), f2{(float)i, (float)m}), r, 8 * t, 8 * m * 256, 3);
+        } else p[t + m * 256] = f2{(float)i, (float)m};
+      }
+    } else {
+      f4* p = reinterpret_cast<f4*>(base);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        if (NT == 1) __builtin_nontemporal_store(f4{(float)i, (float)m, 1.f, 2.f}, p + t + m * 256);
+        else p[t + m * 256] = f4{(float)i, (float)m, 1.f, 2.f};
+      }
+    }
+  }
+}
+
+// linear sweep, one WG = 256 threads x K dwordx4 stores, consecutive WGs consecutive chunks
+template <int K>
+__global__ void __launch_bounds__(256) lin_kernel(f4* out) {
+  f4* p = out + (long long)blockIdx.x * 256 * K + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k * 256] = f4{1.f, 2.f, 3.f, (float)k};
+}
+
+// CWT-like ownership (WG owns R consecutive 32 KB rows) with a bounded number of
+// outstanding stores per wave: s_waitcnt vmcnt(W) after each store
+template <int W, int R>
+__global__ void __launch_bounds__(256) own_wait_kernel(f2* out) {
+  const int t = threadIdx.x;
+  for (int i = 0; i < R; ++i) {
+    f2* p = out + ((long long)blockIdx.x * R + i) * 4096;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      p[t + m * 256] = f2{(float)i, (float)m};
+      if (W == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (W == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if (W == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (W == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
+  }
+}
+// grid-stride linear: K dwordx4 stores per thread, consecutive stores one grid apart
+template <int K>
+__global__ void __launch_bounds__(256) lin_gs_kernel(f4* out, long long stride) {
+  f4* p = out + (long long)blockIdx.x * 256 + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k * stride] = f4{1.f, 2.f, 3.f, (float)k};
+}
+
+int main() {
+  const size_t bytes = NROWS * (size_t)ROWB;
+  char* d;
+  if (hipMalloc(&d, bytes) != hipSuccess) return 1;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  struct Cfg { const char* name; int vec, mode, nwg, nt; };
+  std::vector<Cfg> cfgs = {{"own64rows_x2", 2, 0, 2048, 0}, {"own64rows_x4", 4, 0, 2048, 0},
+                           {"own64rows_x2_nt", 2, 0, 2048, 1}, {"own64rows_x4_nt", 4, 0, 2048, 1},
+                           {"own64rows_x2_buf_aux3", 2, 0, 2048, 2},
+                           {"own16rows_x2", 2, 0, 8192, 0}, {"interleave_x2_768", 2, 1, 768, 0},
+                           {"linear_x2", 2, 0, 131072, 0}, {"linear_x4", 4, 0, 131072, 0},
+                           {"linear_x4_nt", 4, 0, 131072, 1}, {"linear_x2_nt", 2, 0, 131072, 1}};
+  for (int rep = 0; rep < 2; ++rep)
+    for (auto& c : cfgs) {
+      const int rpw = (int)((NROWS + c.nwg - 1) / c.nwg);
+      float best = 1e30f;
+      for (int k = 0; k < 5; ++k) {
+        hipEventRecord(e0);
+        if (c.vec == 2 && c.nt == 0) hipLaunchKernelGGL((rows_kernel<2, 0>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
+        else if (c.vec == 2 && c.nt == 1) hipLaunchKernelGGL((rows_kernel<2, 1>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
+        else if (c.vec == 2) hipLaunchKernelGGL((rows_kernel<2, 2>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
+        else if (c.nt == 1) hipLaunchKernelGGL((rows_kernel<4, 1>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
+        else hipLaunchKernelGGL((rows_kernel<4, 0>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best) best = ms;
+      }
+      if (rep) printf("%-22s %8.3f ms  %7.0f GB/s\n", c.name, best, bytes / best / 1e6);
+    }
+  for (int rep = 0; rep < 2; ++rep) {
+    auto run = [&](const char* name, auto launch) {
+      float best = 1e30f;
+      for (int k = 0; k < 5; ++k) {
+        hipEventRecord(e0);
+        launch();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best) best = ms;
+      }
+      if (rep) printf("%-22s %8.3f ms  %7.0f GB/s\n", name, best, bytes / best / 1e6);
+    };
+    f4* o = reinterpret_cast<f4*>(d);
+    const long long n4 = bytes / 16;
+    run("lin_k1", [&] { hipLaunchKernelGGL(lin_kernel<1>, dim3(n4 / 256), dim3(256), 0, 0, o); });
+    run("lin_k2", [&] { hipLaunchKernelGGL(lin_kernel<2>, dim3(n4 / 512), dim3(256), 0, 0, o); });
+    run("lin_k4", [&] { hipLaunchKernelGGL(lin_kernel<4>, dim3(n4 / 1024), dim3(256), 0, 0, o); });
+    run("lin_k8", [&] { hipLaunchKernelGGL(lin_kernel<8>, dim3(n4 / 2048), dim3(256), 0, 0, o); });
+    run("lin_k16", [&] { hipLaunchKernelGGL(lin_kernel<16>, dim3(n4 / 4096), dim3(256), 0, 0, o); });
+    run("lin_gs_k2", [&] { hipLaunchKernelGGL(lin_gs_kernel<2>, dim3(n4 / 512), dim3(256), 0, 0, o, n4 / 2); });
+    run("lin_gs_k8", [&] { hipLaunchKernelGGL(lin_gs_kernel<8>, dim3(n4 / 2048), dim3(256), 0, 0, o, n4 / 8); });
+    f2* o2 = reinterpret_cast<f2*>(d);
+    run("own64_wait0", [&] { hipLaunchKernelGGL((own_wait_kernel<0, 64>), dim3(2048), dim3(256), 0, 0, o2); });
+    run("own64_wait2", [&] { hipLaunchKernelGGL((own_wait_kernel<2, 64>), dim3(2048), dim3(256), 0, 0, o2); });
+    run("own64_wait4", [&] { hipLaunchKernelGGL((own_wait_kernel<4, 64>), dim3(2048), dim3(256), 0, 0, o2); });
+    run("own64_wait8", [&] { hipLaunchKernelGGL((own_wait_kernel<8, 64>), dim3(2048), dim3(256), 0, 0, o2); });
+    run("own64_nowait", [&] { hipLaunchKernelGGL((own_wait_kernel<99, 64>), dim3(2048), dim3(256), 0, 0, o2); });
+    run("own1_nowait", [&] { hipLaunchKernelGGL((own_wait_kernel<99, 1>), dim3(131072), dim3(256), 0, 0, o2); });
+    run("own4_nowait", [&] { hipLaunchKernelGGL((own_wait_kernel<99, 4>), dim3(32768), dim3(256), 0, 0, o2); });
+  }
+  hipFree(d);
+  return 0;
+}

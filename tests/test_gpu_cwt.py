@@ -53,6 +53,30 @@ def test_cwt_rows_match_oracle(n0, dj, J):
     np.testing.assert_allclose(Sg, P * ss[None, :, None], rtol=1e-6)
 
 
+@pytest.mark.parametrize("n0,dj,J,offset", [(4096, 1 / 12, 127, 0.0), (4096, 1 / 12, 127, 500.0),
+                                            (8192, 1 / 24, 255, 0.0), (2000, 1 / 12, 110, 50.0)])
+def test_band_pruned_rows(n0, dj, J, offset, monkeypatch):
+    """Rows whose filtered spectrum lies in bins [0, N/16^q) enter the inverse FFT at pass q
+    (cwt_common.hpp band_regime).  Random walks with a large mean put most of the energy at
+    the lowest bins -- the worst case for the dropped negative-frequency tail."""
+    rng = np.random.default_rng(n0 + 7)
+    B = 2
+    x = np.stack([red_series(rng, n0) for _ in range(B)]).astype(np.float64)
+    x[1] = np.cumsum(rng.standard_normal(n0)) + offset
+    x = x.astype(np.float32)
+    dt, s0 = 1 / 12, 2 / 12
+    sj = _scales(n0, dt, dj, s0, J)
+    xd = torch.tensor(x, device="cuda")
+    monkeypatch.setenv("WTMI_CWT_PRUNE", "0")
+    full = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
+    monkeypatch.setenv("WTMI_CWT_PRUNE", "1")
+    pr = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
+    assert row_relerr(pr.astype(np.complex128), full.astype(np.complex128)).max() < TOL
+    for b in range(B):
+        ref = pc.cwt(x[b].astype(np.float64), dt, dj, s0, J)[0]
+        assert row_relerr(pr[b].astype(np.complex128), ref).max() < TOL, b
+
+
 def test_many_scales_span_several_chunks():
     rng = np.random.default_rng(99)
     n0, dt, dj, s0, J = 300, 1 / 12, 1 / 64, 2 / 12, 600  # S = 601 > 512-row chunk table

@@ -82,10 +82,36 @@ __device__ __forceinline__ void store_any(const cpx (&v)[16], const CwtArgs& a, 
   }
 }
 
-template <int LOGN, int NBUF, int MODE>
-__global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 : CwtGeom<LOGN, MODE>::MINW)) cwt_morlet_kernel(CwtArgs a) {
+// W row of one scale: Morlet filter + inverse FFT, entering the FFT at pass q when the
+// filtered spectrum is confined to bins [0, N/16^q) (band_regime / band_entry).
+template <int LOGN, int NBUF, bool TWL>
+__device__ __forceinline__ void inverse_row(cpx (&v)[16], const cpx (&X)[16], cpx prm, float f0,
+                                            int q, cpx* my, int bufstride, const cpx* tw, int t,
+                                            int& par, const float4* twl) {
   using P = FftPlan<LOGN>;
-  using G = CwtGeom<LOGN, MODE>;
+  if constexpr (NBUF == 1 && P::P16 >= 2 && (P::NT % 16) == 0) {
+    if (q >= 1) {
+      const cpx y = morlet_bin0(X[0], prm, f0, t);
+      if constexpr (P::P16 >= 3 && (P::NT % 256) == 0) {
+        if (q >= 2) {
+          band_entry<LOGN, 2>(v, y, my, t);
+          fft_row<LOGN, 1, NBUF, TWL, 2>(v, my, bufstride, tw, t, par, twl);
+          return;
+        }
+      }
+      band_entry<LOGN, 1>(v, y, my, t);
+      fft_row<LOGN, 1, NBUF, TWL, 1>(v, my, bufstride, tw, t, par, twl);
+      return;
+    }
+  }
+  morlet_filter<LOGN>(v, X, prm, f0, t);
+  fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
+}
+
+template <int LOGN, int NBUF, int MODE, int VAR = 0>
+__global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 ? 2 : CwtGeom<LOGN, MODE, VAR>::MINW)) cwt_morlet_kernel(CwtArgs a) {
+  using P = FftPlan<LOGN>;
+  using G = CwtGeom<LOGN, MODE, VAR>;
   // per-scale table (alpha, log2 c, 1/signif, -) in LDS: the scale loop must not issue
   // global loads -- a load's vmcnt wait would also wait for every store of the
   // previous row (loads and stores retire in order on the same counter).
@@ -105,9 +131,11 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
   constexpr int bufstride = G::ROWS * P::PADN;
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
-    const cpx mp = morlet_params(a.scales[j0 + i], a.dt, P::N);
+    const double s = a.scales[j0 + i];
+    const cpx mp = morlet_params(s, a.dt, P::N);
     const float sg = a.sigscale ? static_cast<float>(a.sigscale[j0 + i]) : 0.f;
-    prm_tab[i] = make_float4(mp.x, mp.y, sg, 0.f);
+    const int q = (a.prune && NBUF == 1) ? band_regime<LOGN>(s, a.dt, a.f0) : 0;
+    prm_tab[i] = make_float4(mp.x, mp.y, sg, static_cast<float>(q));
   }
 
   constexpr bool TWL = G::TWL;
@@ -121,13 +149,19 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
   }
   int par = 0;
 
+  __shared__ float red[G::BLOCK / kWave];
   cpx X[16];
   load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
+  const float mu = demean_row<LOGN>(X, a.n0, t, red);
   fft_row<LOGN, -1, NBUF, TWL>(X, my, bufstride, tw, t, par, twl);
+  add_mean_spectrum<LOGN>(X, mu, a.n0, t);
   cpx X2[MODE == 1 ? 16 : 1];
   if constexpr (MODE == 1) {
     load_series<LOGN>(X2, a.x2, a.affine2, b, a.ld, a.n0, t);
+    __syncthreads();  // red reuse
+    const float mu2 = demean_row<LOGN>(X2, a.n0, t, red);
     fft_row<LOGN, -1, NBUF, TWL>(X2, my, bufstride, tw, t, par, twl);
+    add_mean_spectrum<LOGN>(X2, mu2, a.n0, t);
   }
   __syncthreads();  // prm_tab visible (the FFT barriers may be absent for N = 16)
 
@@ -141,19 +175,31 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE>::BLOCK), (NBUF == 2 ? 2 :
     const bool valid = jl < j1 - j0;
     const float4 prm4 = prm_tab[valid ? jl : 0];
     const cpx prm = mkc(prm4.x, prm4.y);
+    // the iteration's band regime: the narrowest-band common to its rows (workgroup-uniform,
+    // the transforms contain barriers)
+    int q = 3;
+#pragma unroll
+    for (int gg = 0; gg < G::ROWS; ++gg) {
+      const int jj = it * G::ROWS + gg;
+      if (jj < j1 - j0) q = min(q, static_cast<int>(prm_tab[jj].w));
+    }
     cpx v[16];
-    morlet_filter<LOGN>(v, X, prm, f0, t);
-    fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
+    if (a.diag & 1) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = X[m] * prm.x;
+    } else {
+      inverse_row<LOGN, NBUF, TWL>(v, X, prm, f0, q, my, bufstride, tw, t, par, twl);
+    }
     if constexpr (MODE == 1) {
       cpx w1[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) w1[m] = v[m];
-      morlet_filter<LOGN>(v, X2, prm, f0, t);
-      fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
+      inverse_row<LOGN, NBUF, TWL>(v, X2, prm, f0, q, my, bufstride, tw, t, par, twl);
 #pragma unroll
       for (int m = 0; m < 16; ++m) v[m] = cmul(w1[m], cconj(v[m]));
     }
     if (!valid) continue;
+    if ((a.diag & 2) && v[0].x != -1.2345e30f) continue;
     const int j = j0 + jl;
     const long long rowbase = (b * a.S + j) * static_cast<long long>(a.n0);
     const float sg = prm4.z;
@@ -232,9 +278,9 @@ static int env_int(const char* name, int dflt) {
   return s ? atoi(s) : dflt;
 }
 
-template <int LOGN, int NBUF, int MODE>
+template <int LOGN, int NBUF, int MODE, int VAR = 0>
 static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
-  using G = CwtGeom<LOGN, MODE>;
+  using G = CwtGeom<LOGN, MODE, VAR>;
   // Scale chunking: enough workgroups to fill 256 CUs several times, while keeping
   // at least 4 row-iterations per workgroup to amortise the forward FFT.
   const int rows = G::ROWS;
@@ -252,9 +298,11 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   nch = (a.S + chunk - 1) / chunk;
   a.nchunks = nch;
   a.chunk = chunk;
+  a.prune = env_int("WTMI_CWT_PRUNE", 1);
+  a.diag = env_int("WTMI_CWT_DIAG", 0);
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  hipLaunchKernelGGL((cwt_morlet_kernel<LOGN, NBUF, MODE>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((cwt_morlet_kernel<LOGN, NBUF, MODE, VAR>), dim3(static_cast<unsigned>(grid)),
                      dim3(G::BLOCK), 0, st, a);
   return launch_status();
 }

@@ -24,19 +24,22 @@ struct CwtArgs {
   float* out_u;
   float* out_v;
   int nchunks, chunk;
+  int prune;             // allow band-pruned inverse transforms (band_regime); 0 = full FFTs
+  int diag;              // diagnostics only (WTMI_CWT_DIAG): 1 = skip the inverse FFTs, 2 = skip stores
 };
 
 constexpr double kPi = 3.14159265358979323846;
 constexpr float kLog2e = 1.44269504088896340736f;
 
-template <int LOGN, int MODE>
+template <int LOGN, int MODE, int VAR = 0>
 struct CwtGeom {
   using P = FftPlan<LOGN>;
   static constexpr int ROWS = P::NT >= 256 ? 1 : 256 / P::NT;
   static constexpr int BLOCK = P::NT * ROWS;
   // LOGN >= 13 keeps the radix-16 twiddles in an LDS table (FftPlan::TWL_E): that is
   // what brings the single-series kernel to <= 128 VGPRs, i.e. two 512-thread
-  // workgroups per CU (LDS 2 x 80 KiB) instead of one.
+  // workgroups per CU (LDS 2 x 80 KiB) instead of one.  VAR: launch variants for A/B
+  // sweeps (none at present; LDS twiddles or 4 waves/SIMD at LOGN 12 measured equal, r01).
   static constexpr bool TWL = LOGN >= 13;
   // waves per SIMD requested from the register allocator (4 -> <= 128 VGPRs,
   // 3 -> <= 168, 2 -> <= 256).  A 1024-thread block is 4 waves per SIMD by itself.
@@ -71,6 +74,65 @@ __device__ __forceinline__ void load_series(cpx (&v)[16], const float* __restric
   }
 }
 
+// Mean removal around the forward FFT.  pycwt.cwt transforms the raw series (no
+// centring), and a large offset costs fp32 accuracy in every bin: the FFT's rounding
+// error scales with ||x||, the offset's energy included.  The kernels therefore transform
+// x - mu (mu = the row mean) and add mu's spectrum back exactly:
+//   D[k] = sum_{n < n0} exp(-2 pi i k n / N) = exp(-i pi k (n0-1)/N) sin(pi k n0/N) / sin(pi k/N)
+// (D = N delta_k0 when n0 = N).  mu is bitwise identical in every thread of the row (the
+// xor-butterfly sums are commutative pairwise), so subtraction and correction agree.
+// red: >= BLOCK/64 floats of LDS.  Every thread of the workgroup must call this.
+template <int LOGN>
+__device__ __forceinline__ float demean_row(cpx (&v)[16], int n0, int t, float* red) {
+  using P = FftPlan<LOGN>;
+  float s = 0.f;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) s += v[m].x;  // padding entries are zero
+  constexpr int W = P::NT < kWave ? P::NT : kWave;
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) s += __shfl_xor(s, o, W);
+  if constexpr (P::NT > kWave) {
+    constexpr int WPR = P::NT / kWave;  // waves per row
+    const int wv = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) red[wv] = s;
+    __syncthreads();
+    const int w0 = wv & ~(WPR - 1);
+    s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPR; ++w) s += red[w0 + w];
+  }
+  const float mu = s / static_cast<float>(n0);
+#pragma unroll
+  for (int m = 0; m < 16; ++m)
+    if (t + m * P::NT < n0) v[m].x -= mu;
+  return mu;
+}
+
+// X[k] += mu * D[k] for the 16 bins k = t + m*NT this thread holds (forward spectrum).
+template <int LOGN>
+__device__ __forceinline__ void add_mean_spectrum(cpx (&X)[16], float mu, int n0, int t) {
+  using P = FftPlan<LOGN>;
+  if (n0 == P::N) {
+    if (t == 0) X[0].x += mu * static_cast<float>(P::N);
+    return;
+  }
+  constexpr int N2 = 2 * P::N;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int k = t + m * P::NT;
+    if (k == 0) {
+      X[m].x += mu * static_cast<float>(n0);
+      continue;
+    }
+    const int ph = static_cast<int>((static_cast<long long>(k) * (n0 - 1)) % N2);
+    const int am = static_cast<int>((static_cast<long long>(k) * n0) % N2);
+    float s1, c1;
+    sincospif(static_cast<float>(ph) / P::N, &s1, &c1);
+    const float r = mu * sinpif(static_cast<float>(am) / P::N) / sinpif(static_cast<float>(k) / P::N);
+    X[m] += cpx{c1, -s1} * r;
+  }
+}
+
 // Per-scale filter constants: e_k = alpha * kk - f0, psi_k = exp2(lc - log2(e)/2 * e_k^2)
 // with alpha = 2 pi s / (N dt) and 2^lc = sqrt(2 pi s / dt) * pi^-1/4 / N (1/N of the IFFT).
 __device__ __forceinline__ cpx morlet_params(double s, double dt, int N) {
@@ -94,6 +156,38 @@ __device__ __forceinline__ void morlet_filter(cpx (&v)[16], const cpx (&X)[16], 
     const float psi = __builtin_amdgcn_exp2f(fmaf(e * K, e, prm.y));
     v[m] = cscale(X[m], psi);
   }
+}
+
+// Band regime of one scale for the inverse transform (see band_entry in fft_lds.hpp):
+// the largest Q in {0, 1, 2} such that the filtered spectrum X * psi_bar vanishes to
+// fp32 precision outside bins [0, N/16^Q).  psi_k = exp(-(alpha k - f0)^2 / 2):
+//  - upper edge: bins k >= N/16^Q have alpha k - f0 >= kBandT, psi <= exp(-kBandT^2/2) = 6.8e-10;
+//  - negative frequencies (k >= N/2 in fftfreq order) have psi <= exp(-f0^2/2), dropped only
+//    for f0 >= kBandF0 (Morlet(6): 1.5e-8 of the peak, far below the fp32 FFT's own rounding).
+// Bin 0 (the mean) is always inside the band.  A pruned row is exact up to those terms.
+constexpr double kBandT = 6.5;
+constexpr double kBandF0 = 5.5;
+
+template <int LOGN>
+__device__ __forceinline__ int band_regime(double s, double dt, double f0) {
+  using P = FftPlan<LOGN>;
+  if (f0 < kBandF0) return 0;
+  const double alpha = s * 2.0 * kPi / (static_cast<double>(P::N) * dt);
+  int q = 0;
+#pragma unroll
+  for (int qq = 1; qq <= 2; ++qq) {
+    if (qq < P::P16 && (P::NT % (1 << (4 * qq))) == 0 &&
+        alpha * static_cast<double>(P::N >> (4 * qq)) - f0 >= kBandT)
+      q = qq;
+  }
+  return q;
+}
+
+// Filtered bin t of a band-pruned row (thread t's m = 0 element, frequency index t >= 0).
+__device__ __forceinline__ cpx morlet_bin0(cpx X0, cpx prm, float f0, int t) {
+  constexpr float K = -0.5f * kLog2e;
+  const float e = fmaf(prm.x, static_cast<float>(t), -f0);
+  return cscale(X0, __builtin_amdgcn_exp2f(fmaf(e * K, e, prm.y)));
 }
 
 }  // namespace wtmi

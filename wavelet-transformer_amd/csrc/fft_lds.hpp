@@ -311,15 +311,20 @@ __device__ __forceinline__ void tail_butterflies(cpx* v, const cpx* b) {
 // when NBUF == 2.  par: running buffer parity (NBUF == 2), shared by all calls of
 // the workgroup in the same order.  Every thread of the workgroup must call this
 // the same number of times (it contains __syncthreads()).
-template <int LOGN, int DIR, int NBUF, bool TWL = false>
+//
+// START > 0 enters at radix-16 pass START with v[r] already holding that pass's
+// inputs (band-pruned inverse transforms, see band_entry below); the passes before
+// it are skipped.
+template <int LOGN, int DIR, int NBUF, bool TWL = false, int START = 0>
 __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int bufstride,
                                         const cpx* tw, int t, int& par,
                                         const float4* twl = nullptr) {
   using P = FftPlan<LOGN>;
+  static_assert(START == 0 || (START < P::P16 && NBUF == 1), "pruned entry: radix-16 pass, 1 buffer");
   constexpr bool kAligned = (P::NT % 32) == 0;  // strides are multiples of 32 -> pad is additive
-  dft16<DIR>(v);
-  if constexpr (P::NPASS == 1) return;
-  {
+  if constexpr (START == 0) {
+    dft16<DIR>(v);
+    if constexpr (P::NPASS == 1) return;
     cpx* buf = lds + (NBUF == 2 ? par * bufstride : 0);
     if constexpr (NBUF == 1) __syncthreads();
     cpx* w = buf + 16 * t + (t >> 1);  // lpad(16 t + r) = 16 t + t/2 + r  (r < 16)
@@ -328,21 +333,23 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
     __syncthreads();
   }
   const int pt = lpad(t);
-  int ns = 16;
 #pragma unroll
-  for (int p = 1; p < P::NPASS; ++p) {
+  for (int p = (START > 1 ? START : 1); p < P::NPASS; ++p) {
+    const int ns = 1 << (4 * p);
     const bool last = (p == P::NPASS - 1);
     const cpx* rbuf = lds + (NBUF == 2 ? par * bufstride : 0);
     if (p < P::P16) {
-      if constexpr (kAligned) {
-        const cpx* rb = rbuf + pt;
+      if (p != START) {
+        if constexpr (kAligned) {
+          const cpx* rb = rbuf + pt;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = rb[r * (P::NT + P::NT / 32)];
-      } else {
+          for (int r = 0; r < 16; ++r) v[r] = rb[r * (P::NT + P::NT / 32)];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = rbuf[lpad(t + r * P::NT)];
+          for (int r = 0; r < 16; ++r) v[r] = rbuf[lpad(t + r * P::NT)];
+        }
+        if constexpr (NBUF == 2) par ^= 1;
       }
-      if constexpr (NBUF == 2) par ^= 1;
       if constexpr (TWL)
         apply_tw16_lds<DIR, P::TWL_E>(v, twl, twl_base(p) + (t & (ns - 1)));
       else
@@ -361,7 +368,6 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
           for (int r = 0; r < 16; ++r) wb[16 * r + (r >> 1)] = v[r];
         }
         __syncthreads();
-        ns *= 16;
       }
     } else {
       constexpr int R = P::REM > 1 ? P::REM : 16;
@@ -390,6 +396,29 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
       for (int m = 0; m < 16; ++m) v[m] = o[m];
     }
   }
+}
+
+// Band-pruned entry (inverse transforms of spectra that vanish outside bins [0, N/16^Q)).
+// If only bins k < N/16^Q are non-zero, passes 0..Q-1 of fft_row merely replicate
+// values: pass Q's input at thread t is, for r = 0..15,
+//   v[r] = x[(t >> 4Q) + r * (NT >> 4Q)]
+// (pass p writes its 16 outputs to idxD = (t / 16^p) 16^(p+1) + t mod 16^p + 16^p r, all equal
+// to the single non-zero input when the band is that narrow).  The caller's thread t holds
+// bin t (its m = 0 element) in y; bins are exchanged through lds[0 .. N/16^Q) (one b64 write
+// per thread, 16 broadcast reads), and fft_row<..., START = Q> takes it from there.
+// Saves Q radix-16 passes (butterflies, twiddles, Q-1 LDS exchanges, 15/16 of one).
+template <int LOGN, int Q>
+__device__ __forceinline__ void band_entry(cpx (&v)[16], cpx y, cpx* __restrict__ lds, int t) {
+  using P = FftPlan<LOGN>;
+  static_assert(Q >= 1 && Q < P::P16 && (P::NT % (1 << (4 * Q))) == 0, "band entry");
+  constexpr int KB = P::N >> (4 * Q);
+  constexpr int STEP = P::NT >> (4 * Q);
+  __syncthreads();  // the previous transform's readers are done with lds
+  if (t < KB) lds[t] = y;
+  __syncthreads();
+  const int base = t >> (4 * Q);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = lds[base + r * STEP];
 }
 
 }  // namespace wtmi

@@ -65,12 +65,15 @@ __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, c
   cpx tw[P::NTW_ALLOC];
   fft_twiddles<LOGN>(tw, t);
   int par = 0;
+  __shared__ float red[G::BLOCK / kWave];
   cpx X[16];
   if (which == 0)
     load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
   else
     load_series<LOGN>(X, a.x2, a.affine2, b, a.ld, a.n0, t);
+  const float mu = demean_row<LOGN>(X, a.n0, t, red);
   fft_row<LOGN, -1, 1>(X, lds + g * P::PADN, 0, tw, t, par);
+  add_mean_spectrum<LOGN>(X, mu, a.n0, t);
   if (!valid) return;
   cpx* o = spec + (2 * b + which) * static_cast<long long>(P::N);
 #pragma unroll
