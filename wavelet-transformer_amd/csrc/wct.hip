@@ -117,17 +117,191 @@ __device__ __forceinline__ void put_row(T* row, int t, int n0, F&& val) {
   }
 }
 
+// Regime of the time smoother F_k = exp(-(sn k)^2 / 2) (sn = (s/dt) 2 pi / N): the largest
+// Q in {1, 2} with F <= exp(-kBandT^2/2) for |k| >= K0 = N / 2^(4Q+1), else 0.  A smoothed row
+// of regime Q has its spectrum in [-K0, K0): shifted by K0 it lies in [0, N/16^Q), and the
+// inverse transform enters at pass Q (band_entry) with a time phasor exp(-2 pi i K0 n / N)
+// undoing the shift (K0 is a multiple of 16, so the phasor depends on t only).
+template <int LOGN>
+__device__ __forceinline__ int smooth_regime(double sn) {
+  using P = FftPlan<LOGN>;
+  int q = 0;
+#pragma unroll
+  for (int qq = 1; qq <= 2; ++qq) {
+    const int k0 = P::N >> (4 * qq + 1);
+    if (qq < P::P16 && (P::NT % (1 << (4 * qq))) == 0 && k0 >= 16 && sn * k0 >= kBandT) q = qq;
+  }
+  return q;
+}
+
+// Band bin of a smoothed row of regime Q >= 1: thread t holds at most one bin of [-K0, K0)
+// (k = t from m = 0, or k = t - NT from m = 15); returns it times F / (N s) and its slot
+// k + K0 in the shifted band [0, 2 K0) (-1: none).
+template <int LOGN, int Q>
+__device__ __forceinline__ cpx smooth_band_bin(const cpx (&v)[16], cpx smt, int t, int& slot) {
+  using P = FftPlan<LOGN>;
+  constexpr int K0 = P::N >> (4 * Q + 1);
+  int k = 0;
+  cpx y = mkc(0.f, 0.f);
+  slot = -1;
+  if (t < K0) {
+    k = t;
+    y = v[0];
+    slot = k + K0;
+  } else if (t >= P::NT - K0) {
+    k = t - P::NT;
+    y = v[15];
+    slot = k + K0;
+  }
+  const float kk = static_cast<float>(k);
+  return cscale(y, smt.y * __builtin_amdgcn_exp2f(smt.x * kk * kk));
+}
+
+// Smoothed row from its band bin: band exchange, inverse FFT from pass Q, time phasor
+// exp(-2 pi i K0 n / N) (K0 a multiple of 16: the same for the 16 positions of a thread).
+template <int LOGN, int Q, bool TWL>
+__device__ __forceinline__ void smooth_from_band(cpx (&v)[16], cpx y, int slot, cpx* my, const cpx* tw,
+                                                 int t, int& par, const float4* twl) {
+  using P = FftPlan<LOGN>;
+  constexpr int K0 = P::N >> (4 * Q + 1);
+  constexpr int STEP = P::NT >> (4 * Q);
+  __syncthreads();
+  if (slot >= 0) my[slot] = y;
+  __syncthreads();
+  const int base = t >> (4 * Q);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = my[base + r * STEP];
+  fft_row<LOGN, 1, 1, TWL, Q>(v, my, 0, tw, t, par, twl);
+  const cpx ph = expi_frac(-K0 * t, P::N);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
+}
+
+// Inverse CWT row of phase A from the pair's spectrum row (global / L2), regime Q.
+template <int LOGN, int Q, bool TWL>
+__device__ __forceinline__ void wct_inverse_row(cpx (&v)[16], const cpx* spec_row, cpx prm, float f0,
+                                                cpx* my, const cpx* tw, int t, int& par,
+                                                const float4* twl) {
+  if constexpr (Q >= 1) {
+    asm volatile("" : "+s"(spec_row));  // keep the one load inside the scale loop
+    band_entry<LOGN, Q>(v, morlet_bin0(spec_row[t], prm, f0, t), my, t);
+    fft_row<LOGN, 1, 1, TWL, Q>(v, my, 0, tw, t, par, twl);
+  } else {
+    load_spec<LOGN>(v, spec_row, t);
+    morlet_filter<LOGN>(v, v, prm, f0, t);
+    fft_row<LOGN, 1, 1, TWL>(v, my, 0, tw, t, par, twl);
+  }
+}
+
+// Row regime of phase A: the CWT band regime and the smoother's, whichever is smaller.
+template <int LOGN>
+__device__ __forceinline__ int wct_regime(double s, double dt, double f0, double sn) {
+  const int qc = band_regime<LOGN>(s, dt, f0), qs = smooth_regime<LOGN>(sn);
+  return qc < qs ? qc : qs;
+}
+
+// Per-row outputs of the XWT shape from W12 (|W12|^2, angle, arrows).
+template <int LOGN, bool BUF>
+__device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16], long long rowbase, int t) {
+  const int n0 = a.n0;
+  if (a.out_pow) put_row<LOGN, BUF>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w[m]); });
+  if (a.out_sig)  // phase angle
+    put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return atan2f(w[m].y, w[m].x); });
+  if (a.out_u) {
+    put_row<LOGN, BUF>(a.out_u + rowbase, t, n0, [&](int m) {
+      const float r = sqrtf(cabs2(w[m]));
+      return r > 0.f ? w[m].y / r : 0.f;
+    });
+    put_row<LOGN, BUF>(a.out_v + rowbase, t, n0, [&](int m) {
+      const float r = sqrtf(cabs2(w[m]));
+      return r > 0.f ? w[m].x / r : 1.f;
+    });
+  }
+}
+
+struct WctRowCtx {
+  const cpx* spec1;
+  const cpx* spec2;
+  const cpx* prm_tab;
+  const cpx* smt_tab;
+  cpx* TA;
+  cpx* TB;
+  long long b;
+  int j0;
+};
+
+// Phase A rows [r0, r1) of the workgroup's chunk, all of regime Q (one code path per loop:
+// branches between transform variants inside one loop cost the register allocator dearly).
+//   Q = 0: W1, W2 -> z1 = |W1|^2 + i |W2|^2, W12 -> full smoothing transforms of both.
+//   Q >= 1: pruned inverse transforms, and once each forward transform is done only the one
+//   band bin per thread is kept (2 VGPRs), so W12's outputs and transforms run with z1 dead.
+template <int LOGN, bool FULL, int Q, bool TWL>
+__device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, int r0, int r1, cpx* my,
+                                         const cpx* tw, int g, int t, int& par, const float4* twl) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  constexpr bool BUF = FULL && P::NT >= kWave;
+  const float f0 = static_cast<float>(a.f0);
+  const int n0 = a.n0;
+  for (int r = r0; r < r1; r += G::ROWS) {
+    const int jl = r + g;
+    const bool valid = jl < r1;
+    const cpx prm = c.prm_tab[valid ? jl : r0];
+    const cpx smt = c.smt_tab[valid ? jl : r0];
+    cpx w1[16], v[16];
+    wct_inverse_row<LOGN, Q, TWL>(v, c.spec1, prm, f0, my, tw, t, par, twl);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) w1[m] = v[m];
+    wct_inverse_row<LOGN, Q, TWL>(v, c.spec2, prm, f0, my, tw, t, par, twl);
+    const long long rowbase = (c.b * a.S + c.j0 + (valid ? jl : r0)) * static_cast<long long>(n0);
+    // W12 = W1 conj(W2), z1 = |W1|^2 + i |W2|^2, zero past n0 (the reference smooths the
+    // row zero-padded to N)
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int pos = t + m * P::NT;
+      const cpx w12 = cmul(w1[m], cconj(v[m]));
+      const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
+      const bool in = FULL || pos < n0;
+      w1[m] = in ? w12 : mkc(0.f, 0.f);
+      v[m] = in ? z1 : mkc(0.f, 0.f);
+    }
+    fft_row<LOGN, -1, 1, TWL>(v, my, 0, tw, t, par, twl);
+    if constexpr (Q == 0) {
+      smooth_filter<LOGN>(v, smt.x, smt.y, t);
+      fft_row<LOGN, 1, 1, TWL>(v, my, 0, tw, t, par, twl);
+      // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
+      if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      // the XWT-shaped outputs once z1 is dead (only W12 live: no spills around atan2)
+      if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
+      fft_row<LOGN, -1, 1, TWL>(w1, my, 0, tw, t, par, twl);
+      smooth_filter<LOGN>(w1, smt.x, smt.y, t);
+      fft_row<LOGN, 1, 1, TWL>(w1, my, 0, tw, t, par, twl);
+      if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });
+    } else {
+      int zslot, wslot;
+      const cpx zy = smooth_band_bin<LOGN, Q>(v, smt, t, zslot);
+      if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
+      fft_row<LOGN, -1, 1, TWL>(w1, my, 0, tw, t, par, twl);
+      const cpx wy = smooth_band_bin<LOGN, Q>(w1, smt, t, wslot);
+      smooth_from_band<LOGN, Q, TWL>(w1, wy, wslot, my, tw, t, par, twl);
+      if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+      smooth_from_band<LOGN, Q, TWL>(v, zy, zslot, my, tw, t, par, twl);
+      if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+    }
+  }
+}
+
 template <int LOGN, bool FULL>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  constexpr bool BUF = FULL && P::NT >= kWave;
-  __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::MAXCHUNK + G::TWL_F4];
+  __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::MAXCHUNK + G::TWL_F4 + G::MAXCHUNK / 4];
   cpx* lds = reinterpret_cast<cpx*>(lds4);
   cpx* prm_tab = lds + G::ROWS * P::PADN;      // (alpha, log2 c) of the Morlet filter
   cpx* smt_tab = prm_tab + G::MAXCHUNK;        // (beta, 1/(N s)) of the time smoother
   float4* twl = lds4 + (G::ROWS * P::PADN) / 2 + G::MAXCHUNK;
+  int* q_tab = reinterpret_cast<int*>(twl + G::TWL_F4);  // row regimes (wct_regime)
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = tid - g * P::NT;
@@ -138,16 +312,14 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   const int j0 = ch * a.chunk;
   const int j1 = min(a.S, j0 + a.chunk);
   cpx* my = lds + g * P::PADN;
-  constexpr int bufstride = 0;
-  const cpx* spec1 = spec + 2 * b * static_cast<long long>(P::N);
-  const cpx* spec2 = spec1 + P::N;
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const double s = a.scales[j0 + i];
     prm_tab[i] = morlet_params(s, a.dt, P::N);
     const double sn = s / a.dt * 2.0 * kPi / P::N;  // (s/dt) * (2 pi / N)
     smt_tab[i] = mkc(static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn),
-                             static_cast<float>(1.0 / (static_cast<double>(P::N) * s)));
+                     static_cast<float>(1.0 / (static_cast<double>(P::N) * s)));
+    q_tab[i] = a.prune ? wct_regime<LOGN>(s, a.dt, a.f0, sn) : 0;
   }
   constexpr bool TWL = G::TWL;
   cpx tw[TWL ? P::NTW_REG : P::NTW_ALLOC];
@@ -160,62 +332,37 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   int par = 0;
   __syncthreads();
 
-  const float f0 = static_cast<float>(a.f0);
-  const int n0 = a.n0;
-  const int iters = (j1 - j0 + G::ROWS - 1) / G::ROWS;
-  for (int it = 0; it < iters; ++it) {
-    const int jl = it * G::ROWS + g;
-    const bool valid = jl < j1 - j0;
-    const cpx prm = prm_tab[valid ? jl : 0];
-    const cpx smt = smt_tab[valid ? jl : 0];
-    cpx w1[16], v[16];
-    load_spec<LOGN>(w1, spec1, t);
-    morlet_filter<LOGN>(v, w1, prm, f0, t);
-    fft_row<LOGN, 1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) w1[m] = v[m];
-    load_spec<LOGN>(v, spec2, t);
-    morlet_filter<LOGN>(v, v, prm, f0, t);
-    fft_row<LOGN, 1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
-    const int j = j0 + jl;
-    const long long rowbase = (b * a.S + (valid ? j : j0)) * static_cast<long long>(n0);
-    // W12 = W1 conj(W2) -> |W12|^2, angle, arrows (rows of invalid groups are not
-    // stored); then z1 = |W1|^2 + i |W2|^2 and W12, zero past n0 (the reference
-    // smooths the row zero-padded to N)
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int pos = t + m * P::NT;
-      const cpx w12 = cmul(w1[m], cconj(v[m]));
-      const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
-      const bool in = FULL || pos < n0;
-      w1[m] = in ? w12 : mkc(0.f, 0.f);
-      v[m] = in ? z1 : mkc(0.f, 0.f);
-    }
-    fft_row<LOGN, -1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
-    smooth_filter<LOGN>(v, smt.x, smt.y, t);
-    fft_row<LOGN, 1, 1, TWL>(v, my, bufstride, tw, t, par, twl);
-    // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
-    if (valid) put_row<LOGN, BUF>(TA + rowbase, t, n0, [&](int m) { return v[m]; });
-    // the XWT-shaped outputs once z1 is dead (only W12 live: no spills around atan2)
-    if (valid) {
-      if (a.out_pow) put_row<LOGN, BUF>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w1[m]); });
-      if (a.out_sig)  // phase angle
-        put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return atan2f(w1[m].y, w1[m].x); });
-      if (a.out_u) {
-        put_row<LOGN, BUF>(a.out_u + rowbase, t, n0, [&](int m) {
-          const float r = sqrtf(cabs2(w1[m]));
-          return r > 0.f ? w1[m].y / r : 0.f;
-        });
-        put_row<LOGN, BUF>(a.out_v + rowbase, t, n0, [&](int m) {
-          const float r = sqrtf(cabs2(w1[m]));
-          return r > 0.f ? w1[m].x / r : 1.f;
-        });
+  WctRowCtx c;
+  c.spec1 = spec + 2 * b * static_cast<long long>(P::N);
+  c.spec2 = c.spec1 + P::N;
+  c.prm_tab = prm_tab;
+  c.smt_tab = smt_tab;
+  c.TA = TA;
+  c.TB = TB;
+  c.b = b;
+  c.j0 = j0;
+  // runs of equal regime (the table is shared: every thread sees the same runs)
+  const int nrow = j1 - j0;
+  int r0 = 0;
+  while (r0 < nrow) {
+    const int q = q_tab[r0];
+    int r1 = r0 + 1;
+    while (r1 < nrow && q_tab[r1] == q) ++r1;
+    if (q == 0) {
+      wct_rows<LOGN, FULL, 0, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);
+    } else {
+      if constexpr (P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
+        if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
+          if (q >= 2) {
+            wct_rows<LOGN, FULL, 2, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);
+            r0 = r1;
+            continue;
+          }
+        }
+        wct_rows<LOGN, FULL, 1, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);
       }
     }
-    fft_row<LOGN, -1, 1, TWL>(w1, my, bufstride, tw, t, par, twl);
-    smooth_filter<LOGN>(w1, smt.x, smt.y, t);
-    fft_row<LOGN, 1, 1, TWL>(w1, my, bufstride, tw, t, par, twl);
-    if (valid) put_row<LOGN, BUF>(TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+    r0 = r1;
   }
 }
 
@@ -328,6 +475,8 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, hipStream_t s
   nch = (a.S + chunk - 1) / chunk;
   a.nchunks = nch;
   a.chunk = chunk;
+  const char* pe = getenv("WTMI_WCT_PRUNE");
+  a.prune = pe ? atoi(pe) : 1;
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
   if (a.n0 == (1 << LOGN))
