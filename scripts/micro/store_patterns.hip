@@ -66,6 +66,17 @@ __global__ void __launch_bounds__(256) own_wait_kernel(f2* out) {
     }
   }
 }
+// own64 rows, dwordx2, occupancy limited by a dynamic LDS allocation
+__global__ void __launch_bounds__(256) own_lds_kernel(f2* out, int rows) {
+  extern __shared__ float dyn[];
+  const int t = threadIdx.x;
+  if (t == 1000) dyn[0] = 1.f;  // keep the allocation
+  for (int i = 0; i < rows; ++i) {
+    f2* p = out + ((long long)blockIdx.x * rows + i) * 4096;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) p[t + m * 256] = f2{(float)i, (float)m};
+  }
+}
 // grid-stride linear: K dwordx4 stores per thread, consecutive stores one grid apart
 template <int K>
 __global__ void __launch_bounds__(256) lin_gs_kernel(f4* out, long long stride) {
@@ -137,6 +148,9 @@ int main() {
     run("own64_wait8", [&] { hipLaunchKernelGGL((own_wait_kernel<8, 64>), dim3(2048), dim3(256), 0, 0, o2); });
     run("own64_nowait", [&] { hipLaunchKernelGGL((own_wait_kernel<99, 64>), dim3(2048), dim3(256), 0, 0, o2); });
     run("own1_nowait", [&] { hipLaunchKernelGGL((own_wait_kernel<99, 1>), dim3(131072), dim3(256), 0, 0, o2); });
+    run("own64_lds48k_3wg", [&] { hipLaunchKernelGGL(own_lds_kernel, dim3(2048), dim3(256), 48 * 1024, 0, o2, 64); });
+    run("own64_lds36k_4wg", [&] { hipLaunchKernelGGL(own_lds_kernel, dim3(2048), dim3(256), 36 * 1024, 0, o2, 64); });
+    run("own16_lds48k_3wg", [&] { hipLaunchKernelGGL(own_lds_kernel, dim3(8192), dim3(256), 48 * 1024, 0, o2, 16); });
     run("own4_nowait", [&] { hipLaunchKernelGGL((own_wait_kernel<99, 4>), dim3(32768), dim3(256), 0, 0, o2); });
   }
   hipFree(d);

@@ -33,7 +33,7 @@ def _pair(rng, n):
 
 
 @pytest.mark.parametrize("n,dj", [(64, 1 / 8), (256, 1 / 8), (1000, 1 / 8), (1333, 1 / 12),
-                                  (2048, 1 / 8), (8192, 1 / 8)])
+                                  (2048, 1 / 8), (5000, 1 / 8), (8192, 1 / 8), (16384, 1 / 4)])
 def test_wct_matches_oracle(n, dj):
     from wtmi import transforms
     rng = np.random.default_rng(n)
@@ -51,10 +51,12 @@ def test_wct_matches_oracle(n, dj):
     np.testing.assert_allclose(freq, rfreq, rtol=1e-12)
 
 
-def test_wct_fused_power_and_phase_outputs():
-    from wtmi import ops, transforms
+@pytest.mark.parametrize("n,B", [(1000, 3), (8192, 2)])
+def test_wct_fused_power_and_phase_outputs(n, B):
+    """n = 8192 runs the C4 shape: rows of every band regime, the narrowest through the
+    spectral-correlation path of phase A."""
+    from wtmi import ops, transforms  # noqa: F401
     rng = np.random.default_rng(31)
-    n, B = 1000, 3
     pairs = [_pair(rng, n) for _ in range(B)]
     y1 = torch.tensor(np.stack([p[0] for p in pairs]), device="cuda", dtype=torch.float32)
     y2 = torch.tensor(np.stack([p[1] for p in pairs]), device="cuda", dtype=torch.float32)

@@ -398,86 +398,6 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
   }
 }
 
-// fft_row with a runtime (workgroup-uniform) entry pass: one copy of the transform code
-// serves full and band-pruned rows.  Two inlined copies of the FFT in the branches of a
-// scale loop (fft_row<..., START>) more than double the register-allocation pressure of
-// kernels that keep another row live (WCT phase A: 45 spilled VGPRs vs 2).
-template <int LOGN, int DIR, bool TWL = false>
-__device__ __forceinline__ void fft_row_from(cpx (&v)[16], cpx* __restrict__ lds, const cpx* tw,
-                                             int t, int& par, const float4* twl, int start) {
-  using P = FftPlan<LOGN>;
-  constexpr bool kAligned = (P::NT % 32) == 0;
-  if (start == 0) {
-    dft16<DIR>(v);
-    if constexpr (P::NPASS == 1) return;
-    __syncthreads();
-    cpx* w = lds + 16 * t + (t >> 1);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w[r] = v[r];
-    __syncthreads();
-  }
-  const int pt = lpad(t);
-#pragma unroll
-  for (int p = 1; p < P::NPASS; ++p) {
-    const int ns = 1 << (4 * p);
-    const bool last = (p == P::NPASS - 1);
-    if (p < P::P16) {
-      if (p < start) continue;
-      if (p != start) {
-        if constexpr (kAligned) {
-          const cpx* rb = lds + pt;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = rb[r * (P::NT + P::NT / 32)];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = lds[lpad(t + r * P::NT)];
-        }
-      }
-      if constexpr (TWL)
-        apply_tw16_lds<DIR, P::TWL_E>(v, twl, twl_base(p) + (t & (ns - 1)));
-      else
-        apply_tw16<DIR>(v, tw + 4 * (p - 1));
-      dft16<DIR>(v);
-      if (!last) {
-        const int idxD = (t / ns) * ns * 16 + (t & (ns - 1));
-        __syncthreads();
-        cpx* wb = lds + lpad(idxD);
-        if (ns >= 32) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) wb[r * (ns + ns / 32)] = v[r];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) wb[16 * r + (r >> 1)] = v[r];
-        }
-        __syncthreads();
-      }
-    } else {
-      constexpr int R = P::REM > 1 ? P::REM : 16;
-      constexpr int Q = 16 / R;
-      constexpr int tb = TWL ? 0 : 4 * (P::P16 - 1);
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if constexpr (kAligned) {
-            const int off = q * P::NT + r * (P::N / R);
-            v[q * R + r] = lds[pt + off + (off >> 5)];
-          } else {
-            v[q * R + r] = lds[lpad(t + q * P::NT + r * (P::N / R))];
-          }
-        }
-      tail_butterflies<R, DIR, Q>(v, tw + tb);
-      cpx o[16];
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-#pragma unroll
-        for (int r = 0; r < R; ++r) o[q + r * Q] = v[q * R + r];
-#pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = o[m];
-    }
-  }
-}
-
 // Band-pruned entry (inverse transforms of spectra that vanish outside bins [0, N/16^Q)).
 // If only bins k < N/16^Q are non-zero, passes 0..Q-1 of fft_row merely replicate
 // values: pass Q's input at thread t is, for r = 0..15,
@@ -499,20 +419,6 @@ __device__ __forceinline__ void band_entry(cpx (&v)[16], cpx y, cpx* __restrict_
   const int base = t >> (4 * Q);
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = lds[base + r * STEP];
-}
-
-// band_entry with a runtime Q >= 1 (for fft_row_from).
-template <int LOGN>
-__device__ __forceinline__ void band_entry_dyn(cpx (&v)[16], cpx y, cpx* __restrict__ lds, int t, int q) {
-  using P = FftPlan<LOGN>;
-  const int kb = P::N >> (4 * q);
-  const int step = P::NT >> (4 * q);
-  __syncthreads();
-  if (t < kb) lds[t] = y;
-  __syncthreads();
-  const int base = t >> (4 * q);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = lds[base + r * step];
 }
 
 }  // namespace wtmi

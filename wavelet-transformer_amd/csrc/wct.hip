@@ -226,6 +226,7 @@ struct WctRowCtx {
   const cpx* smt_tab;
   cpx* TA;
   cpx* TB;
+  cpx* band;  // LDS: the band bins A1, A2 of a narrow row (2 * (N >> 8) complex)
   long long b;
   int j0;
 };
@@ -249,11 +250,60 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
     const cpx prm = c.prm_tab[valid ? jl : r0];
     const cpx smt = c.smt_tab[valid ? jl : r0];
     cpx w1[16], v[16];
+    const long long rowbase = (c.b * a.S + c.j0 + (valid ? jl : r0)) * static_cast<long long>(n0);
+    if constexpr (Q == 2 && FULL && G::ROWS == 1) {
+      // Narrow rows: W1, W2 have their spectra A1, A2 in bins [0, KB) and the smoothed fields
+      // theirs in [-K0, K0), 2 K0 = KB.  The forward transforms of z1 and W12 are replaced
+      // by the spectral correlations they equal on a full row (n0 = N):
+      //   FFT(|W1|^2)[k] = N sum_j A1[j] conj(A1[j-k]),  FFT(W1 conj W2)[k] = N sum_j A1[j] conj(A2[j-k]).
+      constexpr int KB = P::N >> 8;
+      constexpr int K0 = KB / 2;
+      const cpx* sp = c.spec1;
+      asm volatile("" : "+s"(sp));  // keep the two loads inside the scale loop
+      const cpx y1 = morlet_bin0(sp[t], prm, f0, t);
+      const cpx y2 = morlet_bin0(sp[P::N + t], prm, f0, t);
+      if (t < KB) {
+        c.band[t] = y1;
+        c.band[KB + t] = y2;
+      }
+      band_entry<LOGN, 2>(w1, y1, my, t);
+      fft_row<LOGN, 1, 1, TWL, 2>(w1, my, 0, tw, t, par, twl);
+      band_entry<LOGN, 2>(v, y2, my, t);
+      fft_row<LOGN, 1, 1, TWL, 2>(v, my, 0, tw, t, par, twl);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) w1[m] = cmul(w1[m], cconj(v[m]));
+      if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
+      cpx zy = mkc(0.f, 0.f), wy = mkc(0.f, 0.f);
+      if (t < KB) {  // output bin k = t - K0 of both smoothed fields, slot t
+        const int k = t - K0;
+        const int jlo = k > 0 ? k : 0, jhi = k < 0 ? KB + k : KB;
+        cpx s11 = mkc(0.f, 0.f), s22 = s11, s12 = s11;
+        for (int jj = jlo; jj < jhi; ++jj) {
+          const cpx a1 = c.band[jj], a2 = c.band[KB + jj];
+          const cpx b1 = cconj(c.band[jj - k]), b2 = cconj(c.band[KB + jj - k]);
+          s11 = cfma(a1.xx, b1, s11);
+          s11 = cfma(a1.yy, mkc(-b1.y, b1.x), s11);
+          s22 = cfma(a2.xx, b2, s22);
+          s22 = cfma(a2.yy, mkc(-b2.y, b2.x), s22);
+          s12 = cfma(a1.xx, b2, s12);
+          s12 = cfma(a1.yy, mkc(-b2.y, b2.x), s12);
+        }
+        const float kk = static_cast<float>(k);
+        const float f = static_cast<float>(P::N) * smt.y * __builtin_amdgcn_exp2f(smt.x * kk * kk);
+        zy = (s11 + mul_i<1>(s22)) * f;  // FFT(|W1|^2 + i |W2|^2) = S11 + i S22
+        wy = s12 * f;
+      }
+      const int slot = t < KB ? t : -1;
+      smooth_from_band<LOGN, 2, TWL>(w1, wy, slot, my, tw, t, par, twl);
+      if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+      smooth_from_band<LOGN, 2, TWL>(v, zy, slot, my, tw, t, par, twl);
+      if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      continue;
+    }
     wct_inverse_row<LOGN, Q, TWL>(v, c.spec1, prm, f0, my, tw, t, par, twl);
 #pragma unroll
     for (int m = 0; m < 16; ++m) w1[m] = v[m];
     wct_inverse_row<LOGN, Q, TWL>(v, c.spec2, prm, f0, my, tw, t, par, twl);
-    const long long rowbase = (c.b * a.S + c.j0 + (valid ? jl : r0)) * static_cast<long long>(n0);
     // W12 = W1 conj(W2), z1 = |W1|^2 + i |W2|^2, zero past n0 (the reference smooths the
     // row zero-padded to N)
 #pragma unroll
@@ -296,7 +346,8 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::MAXCHUNK + G::TWL_F4 + G::MAXCHUNK / 4];
+  constexpr int BAND_F4 = LOGN >= 12 ? (P::N >> 8) : 1;  // 2 * (N >> 8) complex
+  __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::MAXCHUNK + G::TWL_F4 + G::MAXCHUNK / 4 + BAND_F4];
   cpx* lds = reinterpret_cast<cpx*>(lds4);
   cpx* prm_tab = lds + G::ROWS * P::PADN;      // (alpha, log2 c) of the Morlet filter
   cpx* smt_tab = prm_tab + G::MAXCHUNK;        // (beta, 1/(N s)) of the time smoother
@@ -339,6 +390,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   c.smt_tab = smt_tab;
   c.TA = TA;
   c.TB = TB;
+  c.band = reinterpret_cast<cpx*>(q_tab + G::MAXCHUNK);
   c.b = b;
   c.j0 = j0;
   // runs of equal regime (the table is shared: every thread sees the same runs)
