@@ -159,7 +159,7 @@ __device__ __forceinline__ cpx smooth_band_bin(const cpx (&v)[16], cpx smt, int 
 
 // Smoothed row from its band bin: band exchange, inverse FFT from pass Q, time phasor
 // exp(-2 pi i K0 n / N) (K0 a multiple of 16: the same for the 16 positions of a thread).
-template <int LOGN, int Q, bool TWL>
+template <int LOGN, int Q, bool TWL, bool PHASOR = true>
 __device__ __forceinline__ void smooth_from_band(cpx (&v)[16], cpx y, int slot, cpx* my, const cpx* tw,
                                                  int t, int& par, const float4* twl) {
   using P = FftPlan<LOGN>;
@@ -172,9 +172,11 @@ __device__ __forceinline__ void smooth_from_band(cpx (&v)[16], cpx y, int slot, 
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = my[base + r * STEP];
   fft_row<LOGN, 1, 1, TWL, Q>(v, my, 0, tw, t, par, twl);
-  const cpx ph = expi_frac(-K0 * t, P::N);
+  if constexpr (PHASOR) {
+    const cpx ph = expi_frac(-K0 * t, P::N);
 #pragma unroll
-  for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
+    for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
+  }
 }
 
 // Inverse CWT row of phase A from the pair's spectrum row (global / L2), regime Q.
@@ -219,6 +221,54 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
   }
 }
 
+// Per-row plan (wct_plan_kernel), one int per scale row:
+//   bits 0-1  q     band regime of the row's transforms (wct_regime; 0 without pruning)
+//   bit 2     needT the row's time-smoothed fields go to the time-domain workspace (phase B)
+//   bit 3     needS the row's smoothed band spectra go to the band workspace (phase C)
+//   bit 4     spec  output row whose whole boxcar window has q >= 1: its coherence is made by
+//                   phase C from band spectra (no time-domain workspace round trip)
+//   bits 5-6  qw    that window's smallest regime (the union of the members' bands)
+enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5 };
+
+template <int LOGN>
+__device__ __forceinline__ int plan_q(const double* scales, int r, double dt, double f0) {
+  using P = FftPlan<LOGN>;
+  const double s = scales[r];
+  return wct_regime<LOGN>(s, dt, f0, s / dt * 2.0 * kPi / P::N);
+}
+
+// One workgroup; plan[S] = last output row of phase B (the time path), -1 if none.
+template <int LOGN>
+__global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict__ scales, int S, double dt,
+                                                       double f0, int K, int prune, int* __restrict__ plan) {
+  __shared__ int last;
+  if (threadIdx.x == 0) last = -1;
+  __syncthreads();
+  const int LO = K / 2, HI = (K - 1) / 2;
+  auto window = [&](int i, int& qw) {  // all rows of i's window have q >= 1?
+    qw = 3;
+    for (int r = i - LO; r <= i + HI; ++r)
+      if (r >= 0 && r < S) qw = min(qw, plan_q<LOGN>(scales, r, dt, f0));
+    return prune && qw >= 1;
+  };
+  for (int r = threadIdx.x; r < S; r += blockDim.x) {
+    const int q = prune ? plan_q<LOGN>(scales, r, dt, f0) : 0;
+    int qw;
+    const bool spec = window(r, qw);
+    bool needT = false, needS = false;
+    for (int i = r - HI; i <= r + LO; ++i) {  // outputs whose window holds row r
+      if (i < 0 || i >= S) continue;
+      int qi;
+      if (window(i, qi)) needS = true; else needT = true;
+    }
+    plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
+              (spec ? kPlanSpec | (qw << kPlanQwShift) : 0);
+    if (!spec) atomicMax(&last, r);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) plan[S] = last;
+}
+
 struct WctRowCtx {
   const cpx* spec1;
   const cpx* spec2;
@@ -227,6 +277,8 @@ struct WctRowCtx {
   cpx* TA;
   cpx* TB;
   cpx* band;  // LDS: the band bins A1, A2 of a narrow row (2 * (N >> 8) complex)
+  cpx* SB;    // smoothed band spectra [batch][S][2][NT] (index k + NT/2), see wct_plan
+  const int* plan;
   long long b;
   int j0;
 };
@@ -262,6 +314,7 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       asm volatile("" : "+s"(sp));  // keep the two loads inside the scale loop
       const cpx y1 = morlet_bin0(sp[t], prm, f0, t);
       const cpx y2 = morlet_bin0(sp[P::N + t], prm, f0, t);
+      __syncthreads();  // the previous row's correlation reads of c.band are done
       if (t < KB) {
         c.band[t] = y1;
         c.band[KB + t] = y2;
@@ -274,8 +327,10 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       for (int m = 0; m < 16; ++m) w1[m] = cmul(w1[m], cconj(v[m]));
       if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
       cpx zy = mkc(0.f, 0.f), wy = mkc(0.f, 0.f);
-      if (t < KB) {  // output bin k = t - K0 of both smoothed fields, slot t
-        const int k = t - K0;
+      const int k = t - P::NT / 2;  // band-workspace index t <-> bin k
+      const bool holder = k >= -K0 && k < K0;
+      if (holder) {  // bin k of both smoothed fields
+
         const int jlo = k > 0 ? k : 0, jhi = k < 0 ? KB + k : KB;
         cpx s11 = mkc(0.f, 0.f), s22 = s11, s12 = s11;
         for (int jj = jlo; jj < jhi; ++jj) {
@@ -293,11 +348,19 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
         zy = (s11 + mul_i<1>(s22)) * f;  // FFT(|W1|^2 + i |W2|^2) = S11 + i S22
         wy = s12 * f;
       }
-      const int slot = t < KB ? t : -1;
-      smooth_from_band<LOGN, 2, TWL>(w1, wy, slot, my, tw, t, par, twl);
-      if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
-      smooth_from_band<LOGN, 2, TWL>(v, zy, slot, my, tw, t, par, twl);
-      if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      const int pl = c.plan[c.j0 + (valid ? jl : r0)];
+      if (valid && (pl & kPlanNeedS)) {
+        cpx* sb = c.SB + (c.b * a.S + c.j0 + jl) * 2ll * P::NT;
+        sb[t] = zy;
+        sb[P::NT + t] = wy;
+      }
+      if (pl & kPlanNeedT) {
+        const int slot = holder ? k + K0 : -1;
+        smooth_from_band<LOGN, 2, TWL>(w1, wy, slot, my, tw, t, par, twl);
+        if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+        smooth_from_band<LOGN, 2, TWL>(v, zy, slot, my, tw, t, par, twl);
+        if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      }
       continue;
     }
     wct_inverse_row<LOGN, Q, TWL>(v, c.spec1, prm, f0, my, tw, t, par, twl);
@@ -333,17 +396,31 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
       fft_row<LOGN, -1, 1, TWL>(w1, my, 0, tw, t, par, twl);
       const cpx wy = smooth_band_bin<LOGN, Q>(w1, smt, t, wslot);
-      smooth_from_band<LOGN, Q, TWL>(w1, wy, wslot, my, tw, t, par, twl);
-      if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
-      smooth_from_band<LOGN, Q, TWL>(v, zy, zslot, my, tw, t, par, twl);
-      if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      const int pl = c.plan[c.j0 + (valid ? jl : r0)];
+      int pl_any = 0;  // workgroup-uniform (the smoothing transforms hold barriers)
+#pragma unroll
+      for (int gg = 0; gg < G::ROWS; ++gg)
+        if (r + gg < r1) pl_any |= c.plan[c.j0 + r + gg];
+      if (valid && (pl & kPlanNeedS)) {  // thread t holds bin k_t: index k_t + NT/2
+        cpx* sb = c.SB + (c.b * a.S + c.j0 + jl) * 2ll * P::NT;
+        const int ix = (t + P::NT / 2) & (P::NT - 1);
+        sb[ix] = zy;
+        sb[P::NT + ix] = wy;
+      }
+      if (pl_any & kPlanNeedT) {
+        smooth_from_band<LOGN, Q, TWL>(w1, wy, wslot, my, tw, t, par, twl);
+        if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+        smooth_from_band<LOGN, Q, TWL>(v, zy, zslot, my, tw, t, par, twl);
+        if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      }
     }
   }
 }
 
 template <int LOGN, bool FULL>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
-    wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB) {
+    wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB,
+                cpx* __restrict__ SB, const int* __restrict__ plan) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
   constexpr int BAND_F4 = LOGN >= 12 ? (P::N >> 8) : 1;  // 2 * (N >> 8) complex
@@ -370,7 +447,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     const double sn = s / a.dt * 2.0 * kPi / P::N;  // (s/dt) * (2 pi / N)
     smt_tab[i] = mkc(static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn),
                      static_cast<float>(1.0 / (static_cast<double>(P::N) * s)));
-    q_tab[i] = a.prune ? wct_regime<LOGN>(s, a.dt, a.f0, sn) : 0;
+    q_tab[i] = plan[j0 + i] & kPlanQ;
   }
   constexpr bool TWL = G::TWL;
   cpx tw[TWL ? P::NTW_REG : P::NTW_ALLOC];
@@ -391,6 +468,8 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   c.TA = TA;
   c.TB = TB;
   c.band = reinterpret_cast<cpx*>(q_tab + G::MAXCHUNK);
+  c.SB = SB;
+  c.plan = plan;
   c.b = b;
   c.j0 = j0;
   // runs of equal regime (the table is shared: every thread sees the same runs)
@@ -429,7 +508,8 @@ template <> struct ColVec<2> { using T = float4; };
 
 template <int K, int C>
 __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, const cpx* __restrict__ TB,
-                                                   long long batch, int n0, int S, float* __restrict__ coh) {
+                                                   long long batch, int n0, int S, float* __restrict__ coh,
+                                                   const int* __restrict__ plan) {
   using V = typename ColVec<C>::T;
   constexpr int F = 2 * C;  // floats per V
   const int ncol = n0 / C;
@@ -449,13 +529,17 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
   for (int r = 0; r < K; ++r)
 #pragma unroll
     for (int f = 0; f < F; ++f) ra[r][f] = rb[r][f] = 0.f;
-  // row j enters the ring at slot j % K; output row i = j - HI is complete then.
-  for (int jb = 0; jb < S + HI; jb += K) {
+  // row j enters the ring at slot j % K; output row i = j - HI is complete then.  Rows
+  // past the last time-path output (plan[S]) are phase C's: not read, not written.
+  const int last = plan[S];
+  if (last < 0) return;
+  const int jend = last + HI + 1;  // output rows i = j - HI <= last
+  for (int jb = 0; jb < jend; jb += K) {
 #pragma unroll
     for (int r = 0; r < K; ++r) {
       const int j = jb + r;
       if (j < S) {
-        const V a = cola[j * ldv], c = colb[j * ldv];
+        const V a = cola[static_cast<long long>(j) * ldv], c = colb[static_cast<long long>(j) * ldv];
         const float* pa = reinterpret_cast<const float*>(&a);
         const float* pc = reinterpret_cast<const float*>(&c);
 #pragma unroll
@@ -468,7 +552,7 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
         for (int f = 0; f < F; ++f) ra[r][f] = rb[r][f] = 0.f;
       }
       const int i = j - HI;
-      if (i >= 0 && i < S) {
+      if (i >= 0 && i < S && !(plan[i] & kPlanSpec)) {
         float acc[2][F] = {};
 #pragma unroll
         for (int q = 0; q < K; ++q) {
@@ -500,8 +584,111 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
   }
 }
 
+// Phase C: coherence of the output rows whose whole boxcar window consists of band rows
+// (plan bit kPlanSpec).  The scale boxcar is linear, so it is applied to the stored band
+// spectra of the window's rows, and the two sums go through the pruned inverse transform of
+// the window's union band (regime qw):
+//   S1 + i S2 = IFFT(sum_q w_q Z_q),   S12 = IFFT(sum_q w_q W_q),   WCT = |S12|^2 / (S1 S2).
+// These rows skip the time-domain workspace (16 B per coefficient written by phase A and
+// read back by phase B) and phase A's smoothing transforms move here.
+template <int LOGN, int Q, bool BUF, bool TWL>
+__device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __restrict__ SB, int K,
+                                              long long b, int j0, int r0, int r1, cpx* my, const cpx* tw,
+                                              int g, int t, int& par, const float4* twl,
+                                              float* __restrict__ coh) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  constexpr int K0 = P::N >> (4 * Q + 1);
+  const int LO = K / 2;
+  const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
+  const int k = t - P::NT / 2;  // band-workspace index t <-> bin k
+  const bool holder = k >= -K0 && k < K0;
+  for (int r = r0; r < r1; r += G::ROWS) {
+    const int jl = r + g;
+    const bool valid = jl < r1;
+    const int i = j0 + (valid ? jl : r0);
+    cpx yz = mkc(0.f, 0.f), yw = mkc(0.f, 0.f);
+    if (holder) {
+      for (int q = 0; q < K; ++q) {
+        const int rr = i - LO + q;
+        if (rr < 0 || rr >= a.S) continue;
+        const float w = (K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn;
+        const cpx* sb = SB + (b * a.S + rr) * 2ll * P::NT;
+        yz = cfma(cpx{w, w}, sb[t], yz);
+        yw = cfma(cpx{w, w}, sb[P::NT + t], yw);
+      }
+    }
+    const int slot = holder ? k + K0 : -1;
+    // S1 S2 first (16 floats stay live, not 16 complex); |S12|^2 needs no phasor
+    cpx v[16];
+    float den[16];
+    smooth_from_band<LOGN, Q, TWL>(v, yz, slot, my, tw, t, par, twl);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) den[m] = v[m].x * v[m].y;
+    smooth_from_band<LOGN, Q, TWL, false>(v, yw, slot, my, tw, t, par, twl);
+    if (valid) {
+      const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
+      put_row<LOGN, BUF>(coh + rowbase, t, a.n0, [&](int m) { return cabs2(v[m]) / den[m]; });
+    }
+  }
+}
+
+template <int LOGN, bool FULL>
+__global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
+    wct_phase_c(CwtArgs a, const cpx* __restrict__ SB, const int* __restrict__ plan, int K,
+                float* __restrict__ coh) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  constexpr bool BUF = FULL && P::NT >= kWave;
+  __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::TWL_F4];
+  cpx* lds = reinterpret_cast<cpx*>(lds4);
+  float4* twl = lds4 + (G::ROWS * P::PADN) / 2;
+  const int tid = threadIdx.x;
+  const int g = tid / P::NT;
+  const int t = tid - g * P::NT;
+  const long long blk = xcd_remap(blockIdx.x, gridDim.x);
+  const long long b = blk / a.nchunks;
+  const int ch = static_cast<int>(blk - b * a.nchunks);
+  const int j0 = ch * a.chunk;
+  const int j1 = min(a.S, j0 + a.chunk);
+  // any phase-C rows here?  (uniform: every thread reads the same plan entries)
+  bool any = false;
+  for (int r = j0; r < j1; ++r) any |= (plan[r] & kPlanSpec) != 0;
+  if (!any) return;
+  cpx* my = lds + g * P::PADN;
+  constexpr bool TWL = G::TWL;
+  cpx tw[TWL ? P::NTW_REG : P::NTW_ALLOC];
+  if constexpr (TWL) {
+    fft_twiddle_table<LOGN>(twl, tid, G::BLOCK);
+    fft_twiddles_tail<LOGN>(tw, t);
+  } else {
+    fft_twiddles<LOGN>(tw, t);
+  }
+  int par = 0;
+  __syncthreads();
+  const int nrow = j1 - j0;
+  auto key = [&](int r) {
+    const int pl = plan[j0 + r];
+    return (pl & kPlanSpec) ? ((pl >> kPlanQwShift) & 3) : 0;
+  };
+  int r0 = 0;
+  while (r0 < nrow) {
+    const int q = key(r0);
+    int r1 = r0 + 1;
+    while (r1 < nrow && key(r1) == q) ++r1;
+    if constexpr (P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
+      if (q == 1) wct_spec_rows<LOGN, 1, BUF, TWL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
+        if (q == 2) wct_spec_rows<LOGN, 2, BUF, TWL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      }
+    }
+    r0 = r1;
+  }
+}
+
 template <int LOGN>
-static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, hipStream_t st) {
+static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int* plan, int K,
+                          float* coh, hipStream_t st) {
   using G = WctGeom<LOGN>;
   {
     const long long items = 2 * a.batch;
@@ -531,16 +718,26 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, hipStream_t s
   a.prune = pe ? atoi(pe) : 1;
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  if (a.n0 == (1 << LOGN))
-    hipLaunchKernelGGL((wct_phase_a<LOGN, true>), dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, TA, TB);
-  else
-    hipLaunchKernelGGL((wct_phase_a<LOGN, false>), dim3(static_cast<unsigned>(grid)), dim3(G::BLOCK), 0, st, a, spec, TA, TB);
+  hipLaunchKernelGGL(wct_plan_kernel<LOGN>, dim3(1), dim3(256), 0, st, a.scales, a.S, a.dt, a.f0, K,
+                     a.prune, plan);
+  int rc = launch_status();
+  if (rc != kOk) return rc;
+  const dim3 gd(static_cast<unsigned>(grid));
+  if (a.n0 == (1 << LOGN)) {
+    hipLaunchKernelGGL((wct_phase_a<LOGN, true>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, plan);
+    if ((rc = launch_status()) != kOk) return rc;
+    hipLaunchKernelGGL((wct_phase_c<LOGN, true>), gd, dim3(G::BLOCK), 0, st, a, SB, plan, K, coh);
+  } else {
+    hipLaunchKernelGGL((wct_phase_a<LOGN, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, plan);
+    if ((rc = launch_status()) != kOk) return rc;
+    hipLaunchKernelGGL((wct_phase_c<LOGN, false>), gd, dim3(G::BLOCK), 0, st, a, SB, plan, K, coh);
+  }
   return launch_status();
 }
 
 template <int K>
 static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0, int S, float* coh,
-                          hipStream_t st) {
+                          const int* plan, hipStream_t st) {
   const bool pairs = (n0 % 2) == 0;  // 16-byte column pairs need even rows
   const long long ncol = pairs ? n0 / 2 : n0;
   const long long tiles = (ncol + 255) / 256;
@@ -548,10 +745,10 @@ static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0,
   if (grid > 0x7fffffffll) return kErrUnsupported;
   if (pairs)
     hipLaunchKernelGGL((wct_phase_b<K, 2>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
-                       batch, n0, S, coh);
+                       batch, n0, S, coh, plan);
   else
     hipLaunchKernelGGL((wct_phase_b<K, 1>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
-                       batch, n0, S, coh);
+                       batch, n0, S, coh, plan);
   return launch_status();
 }
 
@@ -566,15 +763,24 @@ static int log2_ceil_w(long long n) {
 using namespace wtmi;
 
 // workspace = [T: batch x S x n0 float4][spectra: batch x 2 x N cpx]
+//             [band spectra: batch x S x 2 x N/16 cpx][plan: S + 1 int]
 static long long wct_t_bytes(long long batch, long long n0, int n_scales) {
   const long long b = batch * n0 * static_cast<long long>(n_scales) * static_cast<long long>(sizeof(cpx));
   return 2 * ((b + 255) & ~255ll);
 }
+static long long wct_n(long long n0) { return 1ll << log2_ceil_w(n0 < 1 ? 1 : n0); }
+static long long wct_spec_bytes(long long batch, long long n0) {
+  return (batch * 2 * wct_n(n0) * static_cast<long long>(sizeof(cpx)) + 255) & ~255ll;
+}
+static long long wct_sb_bytes(long long batch, long long n0, int n_scales) {
+  const long long nt = wct_n(n0) / 16 > 0 ? wct_n(n0) / 16 : 1;
+  return (batch * n_scales * 2 * nt * static_cast<long long>(sizeof(cpx)) + 255) & ~255ll;
+}
 
 extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales) {
   if (batch < 0 || n0 < 0 || n_scales < 0) return -1;
-  const long long N = 1ll << log2_ceil_w(n0 < 1 ? 1 : n0);
-  return wct_t_bytes(batch, n0, n_scales) + batch * 2 * N * static_cast<long long>(sizeof(cpx));
+  return wct_t_bytes(batch, n0, n_scales) + wct_spec_bytes(batch, n0) +
+         wct_sb_bytes(batch, n0, n_scales) + 4ll * (n_scales + 1);
 }
 
 extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
@@ -610,10 +816,15 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   const long long plane = wct_t_bytes(batch, n0, n_scales) / 2;
   cpx* TA = static_cast<cpx*>(workspace);
   cpx* TB = reinterpret_cast<cpx*>(static_cast<char*>(workspace) + plane);
-  cpx* spec = reinterpret_cast<cpx*>(static_cast<char*>(workspace) + 2 * plane);
+  char* ws = static_cast<char*>(workspace) + 2 * plane;
+  cpx* spec = reinterpret_cast<cpx*>(ws);
+  ws += wct_spec_bytes(batch, n0);
+  cpx* SB = reinterpret_cast<cpx*>(ws);
+  ws += wct_sb_bytes(batch, n0, n_scales);
+  int* plan = reinterpret_cast<int*>(ws);
   int rc;
   switch (logn) {
-#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, st); break;
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, plan, boxcar, out_coh, st); break;
     WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
     WTMI_A(12) WTMI_A(13) WTMI_A(14)
 #undef WTMI_A
@@ -622,7 +833,7 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   if (rc != kOk) return rc;
   const int n0i = static_cast<int>(n0);
   switch (boxcar) {
-#define WTMI_B(K) case K: return launch_phase_b<K>(TA, TB, batch, n0i, n_scales, out_coh, st);
+#define WTMI_B(K) case K: return launch_phase_b<K>(TA, TB, batch, n0i, n_scales, out_coh, plan, st);
     WTMI_B(1) WTMI_B(2) WTMI_B(3) WTMI_B(4) WTMI_B(5) WTMI_B(6) WTMI_B(7) WTMI_B(8)
     WTMI_B(9) WTMI_B(10) WTMI_B(11) WTMI_B(12) WTMI_B(13) WTMI_B(14) WTMI_B(15) WTMI_B(16)
     WTMI_B(17) WTMI_B(18) WTMI_B(19) WTMI_B(20) WTMI_B(21) WTMI_B(22) WTMI_B(23) WTMI_B(24)
