@@ -275,17 +275,17 @@ __device__ __forceinline__ void apply_tw16_lds(cpx* v, const float4* tab, int id
 template <int R, int DIR, int Q>
 __device__ __forceinline__ void apply_tw_tail(cpx* v, const cpx* b) {
   if constexpr (R == 2) {
-    v[1] = cmul(v[1], rot16<DIR, Q>(twd<DIR>(opaque(b[0]))));
+    v[1] = cmul(v[1], rot16<DIR, Q>(twd<DIR>(b[0])));
   } else if constexpr (R == 4) {
-    const cpx w1 = rot16<DIR, Q>(twd<DIR>(opaque(b[0])));
-    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(opaque(b[1])));
+    const cpx w1 = rot16<DIR, Q>(twd<DIR>(b[0]));
+    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(b[1]));
     v[1] = cmul(v[1], w1);
     v[2] = cmul(v[2], w2);
     v[3] = cmul(v[3], cmul(w1, w2));
   } else {
-    const cpx w1 = rot16<DIR, Q>(twd<DIR>(opaque(b[0])));
-    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(opaque(b[1])));
-    const cpx w4 = rot16<DIR, 4 * Q>(twd<DIR>(opaque(b[2])));
+    const cpx w1 = rot16<DIR, Q>(twd<DIR>(b[0]));
+    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(b[1]));
+    const cpx w4 = rot16<DIR, 4 * Q>(twd<DIR>(b[2]));
     const cpx w3 = cmul(w1, w2);
     v[1] = cmul(v[1], w1);
     v[2] = cmul(v[2], w2);
@@ -385,7 +385,10 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
           }
         }
       if constexpr (NBUF == 2) par ^= 1;
-      tail_butterflies<R, DIR, Q>(v, tw + tb);
+      cpx tbase[P::NTW_REM > 0 ? P::NTW_REM : 1];
+#pragma unroll
+      for (int e = 0; e < P::NTW_REM; ++e) tbase[e] = opaque(tw[tb + e]);
+      tail_butterflies<R, DIR, Q>(v, tbase);
       // register q*R + r holds position t + (q + r*Q)*NT
       cpx o[16];
 #pragma unroll

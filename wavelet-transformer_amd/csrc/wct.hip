@@ -141,6 +141,7 @@ template <int LOGN, int Q>
 __device__ __forceinline__ cpx smooth_band_bin(const cpx (&v)[16], cpx smt, int t, int& slot) {
   using P = FftPlan<LOGN>;
   constexpr int K0 = P::N >> (4 * Q + 1);
+  asm volatile("" : "+v"(t));  // per-row, not hoisted (register budget)
   int k = 0;
   cpx y = mkc(0.f, 0.f);
   slot = -1;
@@ -173,7 +174,9 @@ __device__ __forceinline__ void smooth_from_band(cpx (&v)[16], cpx y, int slot, 
   for (int r = 0; r < 16; ++r) v[r] = my[base + r * STEP];
   fft_row<LOGN, 1, 1, TWL, Q>(v, my, 0, tw, t, par, twl);
   if constexpr (PHASOR) {
-    const cpx ph = expi_frac(-K0 * t, P::N);
+    int tt = t;
+    asm volatile("" : "+v"(tt));  // recompute per row: hoisted, the phasors spill (WCT VGPR budget 128)
+    const cpx ph = expi_frac(-K0 * tt, P::N);
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
   }
@@ -600,13 +603,15 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
   using G = WctGeom<LOGN>;
   constexpr int K0 = P::N >> (4 * Q + 1);
   const int LO = K / 2;
-  const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
-  const int k = t - P::NT / 2;  // band-workspace index t <-> bin k
-  const bool holder = k >= -K0 && k < K0;
   for (int r = r0; r < r1; r += G::ROWS) {
     const int jl = r + g;
     const bool valid = jl < r1;
     const int i = j0 + (valid ? jl : r0);
+    int tt = t;
+    asm volatile("" : "+v"(tt));  // per-row index math, not hoisted (register budget)
+    const int k = tt - P::NT / 2;  // band-workspace index t <-> bin k
+    const bool holder = k >= -K0 && k < K0;
+    const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
     cpx yz = mkc(0.f, 0.f), yw = mkc(0.f, 0.f);
     if (holder) {
       for (int q = 0; q < K; ++q) {
@@ -614,8 +619,8 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
         if (rr < 0 || rr >= a.S) continue;
         const float w = (K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn;
         const cpx* sb = SB + (b * a.S + rr) * 2ll * P::NT;
-        yz = cfma(cpx{w, w}, sb[t], yz);
-        yw = cfma(cpx{w, w}, sb[P::NT + t], yw);
+        yz = cfma(cpx{w, w}, sb[tt], yz);
+        yw = cfma(cpx{w, w}, sb[P::NT + tt], yw);
       }
     }
     const int slot = holder ? k + K0 : -1;
