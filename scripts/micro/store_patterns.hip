@@ -28,6 +28,9 @@ __global__ void __launch_bounds__(256) rows_kernel(char* out, int mode, int nwg,
         else if (NT == 2) {
           __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), f2{(float)i, (float)m}), r, 8 * t, 8 * m * 256, 3);
+        } else if (NT == 3) {
+          __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), f2{(float)i, (float)m}), r, 8 * t, 8 * m * 256, 0);
         } else p[t + m * 256] = f2{(float)i, (float)m};
       }
     } else {
@@ -96,6 +99,7 @@ int main() {
   std::vector<Cfg> cfgs = {{"own64rows_x2", 2, 0, 2048, 0}, {"own64rows_x4", 4, 0, 2048, 0},
                            {"own64rows_x2_nt", 2, 0, 2048, 1}, {"own64rows_x4_nt", 4, 0, 2048, 1},
                            {"own64rows_x2_buf_aux3", 2, 0, 2048, 2},
+                           {"own64rows_x2_buf_aux0", 2, 0, 2048, 3},
                            {"own16rows_x2", 2, 0, 8192, 0}, {"interleave_x2_768", 2, 1, 768, 0},
                            {"linear_x2", 2, 0, 131072, 0}, {"linear_x4", 4, 0, 131072, 0},
                            {"linear_x4_nt", 4, 0, 131072, 1}, {"linear_x2_nt", 2, 0, 131072, 1}};
@@ -107,7 +111,8 @@ int main() {
         hipEventRecord(e0);
         if (c.vec == 2 && c.nt == 0) hipLaunchKernelGGL((rows_kernel<2, 0>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
         else if (c.vec == 2 && c.nt == 1) hipLaunchKernelGGL((rows_kernel<2, 1>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
-        else if (c.vec == 2) hipLaunchKernelGGL((rows_kernel<2, 2>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
+        else if (c.vec == 2 && c.nt == 2) hipLaunchKernelGGL((rows_kernel<2, 2>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
+        else if (c.vec == 2) hipLaunchKernelGGL((rows_kernel<2, 3>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
         else if (c.nt == 1) hipLaunchKernelGGL((rows_kernel<4, 1>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
         else hipLaunchKernelGGL((rows_kernel<4, 0>), dim3(c.nwg), dim3(256), 0, 0, d, c.mode, c.nwg, rpw);
         hipEventRecord(e1);
