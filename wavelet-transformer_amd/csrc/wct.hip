@@ -241,32 +241,34 @@ __device__ __forceinline__ int plan_q(const double* scales, int r, double dt, do
 }
 
 // One workgroup; plan[S] = last output row of phase B (the time path), -1 if none.
+// scratch: 2 S ints (row regimes, then each output row's window regime or -1).
 template <int LOGN>
 __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict__ scales, int S, double dt,
-                                                       double f0, int K, int prune, int* __restrict__ plan) {
+                                                       double f0, int K, int prune, int* __restrict__ plan,
+                                                       int* __restrict__ scratch) {
   __shared__ int last;
   if (threadIdx.x == 0) last = -1;
-  __syncthreads();
   const int LO = K / 2, HI = (K - 1) / 2;
-  auto window = [&](int i, int& qw) {  // all rows of i's window have q >= 1?
-    qw = 3;
-    for (int r = i - LO; r <= i + HI; ++r)
-      if (r >= 0 && r < S) qw = min(qw, plan_q<LOGN>(scales, r, dt, f0));
-    return prune && qw >= 1;
-  };
+  int* qrow = scratch;
+  int* qwin = scratch + S;
+  for (int r = threadIdx.x; r < S; r += blockDim.x) qrow[r] = prune ? plan_q<LOGN>(scales, r, dt, f0) : 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < S; i += blockDim.x) {  // window regime; -1: some member has q = 0
+    int qw = 3;
+    for (int r = max(0, i - LO); r <= min(S - 1, i + HI); ++r) qw = min(qw, qrow[r]);
+    qwin[i] = (prune && qw >= 1) ? qw : -1;
+  }
+  __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
-    const int q = prune ? plan_q<LOGN>(scales, r, dt, f0) : 0;
-    int qw;
-    const bool spec = window(r, qw);
+    const int q = qrow[r];
     bool needT = false, needS = false;
-    for (int i = r - HI; i <= r + LO; ++i) {  // outputs whose window holds row r
-      if (i < 0 || i >= S) continue;
-      int qi;
-      if (window(i, qi)) needS = true; else needT = true;
+    for (int i = max(0, r - HI); i <= min(S - 1, r + LO); ++i) {  // outputs whose window holds r
+      if (qwin[i] >= 1) needS = true; else needT = true;
     }
+    const int qw = qwin[r];
     plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
-              (spec ? kPlanSpec | (qw << kPlanQwShift) : 0);
-    if (!spec) atomicMax(&last, r);
+              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0);
+    if (qw < 1) atomicMax(&last, r);
   }
   __syncthreads();
   if (threadIdx.x == 0) plan[S] = last;
@@ -724,7 +726,7 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int*
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
   hipLaunchKernelGGL(wct_plan_kernel<LOGN>, dim3(1), dim3(256), 0, st, a.scales, a.S, a.dt, a.f0, K,
-                     a.prune, plan);
+                     a.prune, plan, plan + a.S + 1);
   int rc = launch_status();
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
@@ -768,7 +770,7 @@ static int log2_ceil_w(long long n) {
 using namespace wtmi;
 
 // workspace = [T: batch x S x n0 float4][spectra: batch x 2 x N cpx]
-//             [band spectra: batch x S x 2 x N/16 cpx][plan: S + 1 int]
+//             [band spectra: batch x S x 2 x N/16 cpx][plan: S + 1 int][plan scratch: 2 S int]
 static long long wct_t_bytes(long long batch, long long n0, int n_scales) {
   const long long b = batch * n0 * static_cast<long long>(n_scales) * static_cast<long long>(sizeof(cpx));
   return 2 * ((b + 255) & ~255ll);
@@ -785,7 +787,7 @@ static long long wct_sb_bytes(long long batch, long long n0, int n_scales) {
 extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales) {
   if (batch < 0 || n0 < 0 || n_scales < 0) return -1;
   return wct_t_bytes(batch, n0, n_scales) + wct_spec_bytes(batch, n0) +
-         wct_sb_bytes(batch, n0, n_scales) + 4ll * (n_scales + 1);
+         wct_sb_bytes(batch, n0, n_scales) + 4ll * (3 * n_scales + 1);
 }
 
 extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
