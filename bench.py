@@ -158,7 +158,8 @@ class C5(C2):
     """Large-batch CWT: 8192 series/GPU x 8192 x 256 scales (dj = 1/24), streamed in
     chunks of 256 series into a reused output buffer (never fully resident)."""
     name = "c5"
-    B, n0, dj, J, chunk = 8192, 8192, 1 / 24, 255, 256
+    B, n0, dj, J = 8192, 8192, 1 / 24, 255
+    chunk = int(os.environ.get("WTMI_C5_CHUNK", "256"))
 
     def __init__(self, rank, dev):
         import torch
