@@ -219,7 +219,12 @@ __global__ void __launch_bounds__(1024) imodwt_kernel(const float* __restrict__ 
 // of 4, so every tap is one aligned ds_read_b128; levels 1 and 2 read a register
 // window of 3 / 5 aligned float4 blocks and form all taps from it.
 
-template <int L, int DM, bool FWD>
+// Padded LDS index of float4 group q (synthesis V: one pad group per 8).  The dilation-chain
+// mapping puts lanes M = 8 groups apart for dq = 1, a 128-byte stride: an 8-way bank conflict on
+// every ds_read_b128 / ds_write_b128 without the pad (63 % of LDS cycles were conflicts).
+__device__ __forceinline__ int vpad(int q) { return q + (q >> 3); }
+
+template <int L, int DM, bool FWD, bool PAD = false>
 __device__ __forceinline__ void window_taps(const float4* __restrict__ V4, int q, int ng,
                                             const FilterBank& fb, float4& a, float4& b) {
   // FWD: taps at p - DM*l (analysis); else p + DM*l (synthesis).  Window of NB blocks.
@@ -230,7 +235,7 @@ __device__ __forceinline__ void window_taps(const float4* __restrict__ V4, int q
   for (int u = 0; u < NB; ++u) {
     int qs = FWD ? q - (NB - 1) + u : q + u;
     qs = qs < 0 ? qs + ng : (qs >= ng ? qs - ng : qs);
-    const float4 v = V4[qs];
+    const float4 v = V4[PAD ? vpad(qs) : qs];
     f[4 * u] = v.x; f[4 * u + 1] = v.y; f[4 * u + 2] = v.z; f[4 * u + 3] = v.w;
   }
   float ra[4] = {0.f, 0.f, 0.f, 0.f}, rb[4] = {0.f, 0.f, 0.f, 0.f};
@@ -355,7 +360,7 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
 // per thread (GROUPS * 4 * threads >= n).  PREFETCH: the next row W_{j-1} is loaded
 // into registers while level j computes (costs 4*GROUPS VGPRs); otherwise each level
 // starts with a direct global -> LDS copy of W_j.
-template <int L, int GROUPS, int T>
+template <int L, int GROUPS, int T, bool PAD = false>
 __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const float4* __restrict__ W4,
                                           int ng, int dm, float wsel, const FilterBank& fb, int tid,
                                           float4 (&vreg)[GROUPS]) {
@@ -367,10 +372,10 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
       asm volatile("" : "+v"(q));  // keep tap addresses out of LICM (VGPR blow-up)
       float4 av, aw, bw, dummy;
       if (dm == 1) {
-        window_taps<L, 1, false>(V4, q, ng, fb, dummy, av);
+        window_taps<L, 1, false, PAD>(V4, q, ng, fb, dummy, av);
         window_taps<L, 1, false>(W4, q, ng, fb, aw, bw);
       } else {
-        window_taps<L, 2, false>(V4, q, ng, fb, dummy, av);
+        window_taps<L, 2, false, PAD>(V4, q, ng, fb, dummy, av);
         window_taps<L, 2, false>(W4, q, ng, fb, aw, bw);
       }
       vreg[k] = make_float4(fmaf(wsel, aw.x, av.x), fmaf(wsel, aw.y, av.y), fmaf(wsel, aw.z, av.z),
@@ -388,7 +393,7 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
       for (int l = 0; l < L; ++l) {
         int qs = q + (dq * l) % ng;
         if (qs >= ng) qs -= ng;
-        fma4(acc, fb.g[l], V4[qs]);
+        fma4(acc, fb.g[l], V4[PAD ? vpad(qs) : qs]);
         fma4(acc, wsel * fb.h[l], W4[qs]);
       }
       vreg[k] = acc;
@@ -404,7 +409,7 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
 // instead of L (the 8x re-read of W_j through L2 is what bounds the stride-T form).
 // Lanes with consecutive r read consecutive groups: coalesced for dq >= 64 groups,
 // dq-group contiguous runs below that.  Needs ng == M*T and ng % (M*dq) == 0.
-template <int L, int M>
+template <int L, int M, bool PAD = false>
 __device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, const float4* __restrict__ W4,
                                                int ng, int dqlog, const float (&hs)[L],
                                                const FilterBank& fb, int tid, float4 (&vreg)[M]) {
@@ -414,7 +419,10 @@ __device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, co
 #pragma unroll
   for (int k = 0; k < M + L - 1; ++k) wv[k] = W4[(q0 + k * dq) % ng];  // taps may wrap >1x
 #pragma unroll
-  for (int k = 0; k < M + L - 1; ++k) vv[k] = V4[(q0 + k * dq) % ng];
+  for (int k = 0; k < M + L - 1; ++k) {
+    const int qv = (q0 + k * dq) % ng;
+    vv[k] = V4[PAD ? vpad(qv) : qv];
+  }
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -440,10 +448,12 @@ __global__ void __launch_bounds__(T)
     imodwt_vec_kernel(const float* __restrict__ w, int n, int level, FilterBank fb, unsigned long long keep,
                       float* __restrict__ x, long long ld_out) {
   constexpr bool PREFETCH = MODE == 1;
+  constexpr bool PAD = MODE >= 2;  // V alone in LDS: padded (vpad), see window_taps
   extern __shared__ __attribute__((aligned(16))) float4 sm4[];
   const int ng = n >> 2;
   float4* V4 = sm4;
   float4* W4 = sm4 + ng;
+  auto vp = [](int q) { return PAD ? vpad(q) : q; };
   const int tid = threadIdx.x;
   const long long b = blockIdx.x;
   const float* win = w + b * static_cast<long long>(level + 1) * n;
@@ -451,7 +461,7 @@ __global__ void __launch_bounds__(T)
   const bool keepV = (keep >> level) & 1ull;
   {
     const float4* vr = reinterpret_cast<const float4*>(win + static_cast<long long>(level) * n);
-    for (int q = tid; q < ng; q += T) V4[q] = keepV ? vr[q] : z4;
+    for (int q = tid; q < ng; q += T) V4[vp(q)] = keepV ? vr[q] : z4;
   }
   float4 pre[GROUPS];
   if (PREFETCH) {
@@ -486,26 +496,26 @@ __global__ void __launch_bounds__(T)
       float hs[L];
 #pragma unroll
       for (int l = 0; l < L; ++l) hs[l] = wsel * fb.h[l];
-      const int q0 = syn_level_chain<L, GROUPS>(V4, wr, ng, dqlog, hs, fb, tl, vreg);
+      const int q0 = syn_level_chain<L, GROUPS, PAD>(V4, wr, ng, dqlog, hs, fb, tl, vreg);
       __syncthreads();
 #pragma unroll
-      for (int k = 0; k < GROUPS; ++k) V4[q0 + (k << dqlog)] = vreg[k];
+      for (int k = 0; k < GROUPS; ++k) V4[vp(q0 + (k << dqlog))] = vreg[k];
       continue;
     }
-    syn_level<L, GROUPS, T>(V4, MODE >= 2 ? wr : W4, ng, dm, wsel, fb, tl, vreg);
+    syn_level<L, GROUPS, T, PAD>(V4, MODE >= 2 ? wr : W4, ng, dm, wsel, fb, tl, vreg);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < GROUPS; ++k) {
       const int q = tl + k * T;
       if (q < ng) {
-        V4[q] = vreg[k];
+        V4[vp(q)] = vreg[k];
         if (PREFETCH && j > 1) W4[q] = pre[k];
       }
     }
   }
   __syncthreads();
   float4* xo = reinterpret_cast<float4*>(x + b * ld_out);
-  for (int q = tid; q < ng; q += T) xo[q] = V4[q];
+  for (int q = tid; q < ng; q += T) xo[q] = V4[vp(q)];
 }
 
 static int modwt_block(int n) {
@@ -600,6 +610,7 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
       allow_lds(kernel, lds);
       hipLaunchKernelGGL(kernel, dim3(batch), dim3(t), lds, st, w, ni, level, fb, keep_mask, x, ld_out);
     };
+    const size_t lds_pad = (static_cast<size_t>(ni / 4) + ni / 32) * 16;  // vpad'ed V (MODE 2/3)
     auto launch_lds = [&](auto kernel, int t, size_t bytes) {
       allow_lds(kernel, bytes);
       hipLaunchKernelGGL(kernel, dim3(batch), dim3(t), bytes, st, w, ni, level, fb, keep_mask, x, ld_out);
@@ -612,17 +623,17 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
     else if (ng <= 1024)
       launch(imodwt_vec_kernel<8, 1, 1024, 0>, 1024);
     else if (ng <= 2048)
-      launch_lds(imodwt_vec_kernel<8, 2, 1024, 3>, 1024, lds / 2);
+      launch_lds(imodwt_vec_kernel<8, 2, 1024, 3>, 1024, lds_pad);
     else if (var == 1)
       launch(imodwt_vec_kernel<8, 4, 1024, 1>, 1024);
     else if (var == 2)
-      launch_lds(imodwt_vec_kernel<8, 4, 1024, 2>, 1024, lds / 2);
+      launch_lds(imodwt_vec_kernel<8, 4, 1024, 2>, 1024, lds_pad);
     else if (var == 3)
       launch(imodwt_vec_kernel<8, 4, 1024, 0>, 1024);
     else if (var == 4)  // C3 A/B (ms): W from global, 2 WG/CU 2.00; W via LDS 2.11; + register prefetch 2.71
-      launch_lds(imodwt_vec_kernel<8, 8, 512, 2>, 512, lds / 2);
+      launch_lds(imodwt_vec_kernel<8, 8, 512, 2>, 512, lds_pad);
     else
-      launch_lds(imodwt_vec_kernel<8, 8, 512, 3>, 512, lds / 2);
+      launch_lds(imodwt_vec_kernel<8, 8, 512, 3>, 512, lds_pad);
   } else if (n_taps == 8) {
     allow_lds(imodwt_kernel<8>, lds);
     hipLaunchKernelGGL(imodwt_kernel<8>, dim3(batch), dim3(block), lds, st, w, ni, level, n_taps, fb,
