@@ -80,6 +80,36 @@ __global__ void __launch_bounds__(256) own_lds_kernel(f2* out, int rows) {
     for (int m = 0; m < 16; ++m) p[t + m * 256] = f2{(float)i, (float)m};
   }
 }
+// K 4 KB chunks per WG (dwordx4, one per lane per chunk); chunk c of WG w at index
+// ((w / 8) * K + c) * 8 + w % 8: the 8 XCDs interleave at 4 KB granularity while each WG
+// still writes K chunks (XCD = w % 8 under the round-robin dispatch)
+template <int K>
+__global__ void __launch_bounds__(256) xcd_chunks_kernel(f4* out) {
+  const unsigned w = blockIdx.x;
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const long long idx = ((long long)(w / 8) * K + c) * 8 + (w % 8);
+    out[idx * 256 + threadIdx.x] = f4{1.f, 2.f, 3.f, (float)c};
+  }
+}
+// same but each WG's K chunks contiguous (32 KB run for K = 8) and consecutive WGs adjacent
+// (= lin_k8) -- reference
+// CWT-like row ownership (WG owns R consecutive 32 KB rows, 16 x 2 KB steps per row, 4 waves
+// x 512 B per step) with the step order rotated by the workgroup index: concurrent workgroups
+// then write different offsets within their (32 KB-aligned) rows
+template <int R, int ROT>
+__global__ void __launch_bounds__(256) own_rot_kernel(f2* out) {
+  const int t = threadIdx.x;
+  const int rot = ROT ? (blockIdx.x * ROT) & 15 : 0;
+  for (int i = 0; i < R; ++i) {
+    f2* p = out + ((long long)blockIdx.x * R + i) * 4096;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int mm = (m + rot) & 15;
+      p[t + mm * 256] = f2{(float)i, (float)mm};
+    }
+  }
+}
 // grid-stride linear: K dwordx4 stores per thread, consecutive stores one grid apart
 template <int K>
 __global__ void __launch_bounds__(256) lin_gs_kernel(f4* out, long long stride) {
@@ -144,6 +174,16 @@ int main() {
     run("lin_k4", [&] { hipLaunchKernelGGL(lin_kernel<4>, dim3(n4 / 1024), dim3(256), 0, 0, o); });
     run("lin_k8", [&] { hipLaunchKernelGGL(lin_kernel<8>, dim3(n4 / 2048), dim3(256), 0, 0, o); });
     run("lin_k16", [&] { hipLaunchKernelGGL(lin_kernel<16>, dim3(n4 / 4096), dim3(256), 0, 0, o); });
+    run("xcd_k8", [&] { hipLaunchKernelGGL(xcd_chunks_kernel<8>, dim3(n4 / 2048), dim3(256), 0, 0, o); });
+    run("xcd_k32", [&] { hipLaunchKernelGGL(xcd_chunks_kernel<32>, dim3(n4 / 8192), dim3(256), 0, 0, o); });
+    run("lin_k32", [&] { hipLaunchKernelGGL(lin_kernel<32>, dim3(n4 / 8192), dim3(256), 0, 0, o); });
+    {
+      f2* o2r = reinterpret_cast<f2*>(d);
+      run("own64_rot0", [&] { hipLaunchKernelGGL((own_rot_kernel<64, 0>), dim3(2048), dim3(256), 0, 0, o2r); });
+      run("own64_rot1", [&] { hipLaunchKernelGGL((own_rot_kernel<64, 1>), dim3(2048), dim3(256), 0, 0, o2r); });
+      run("own64_rot5", [&] { hipLaunchKernelGGL((own_rot_kernel<64, 5>), dim3(2048), dim3(256), 0, 0, o2r); });
+      run("own64_rot2", [&] { hipLaunchKernelGGL((own_rot_kernel<64, 2>), dim3(2048), dim3(256), 0, 0, o2r); });
+    }
     run("lin_gs_k2", [&] { hipLaunchKernelGGL(lin_gs_kernel<2>, dim3(n4 / 512), dim3(256), 0, 0, o, n4 / 2); });
     run("lin_gs_k8", [&] { hipLaunchKernelGGL(lin_gs_kernel<8>, dim3(n4 / 2048), dim3(256), 0, 0, o, n4 / 8); });
     f2* o2 = reinterpret_cast<f2*>(d);

@@ -130,6 +130,18 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
   cpx* my = lds + g * P::PADN;
   constexpr int bufstride = G::ROWS * P::PADN;
 
+  if (a.diag & 4) {  // diagnostics: the kernel's row stores alone (no tables, no transforms)
+    const int kind = (a.out_w ? kOutW : 0) | (a.out_pow ? kOutPow : 0);
+    for (int jl = g; jl < j1 - j0; jl += G::ROWS) {
+      cpx v[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = mkc(static_cast<float>(jl), static_cast<float>(m));
+      const long long rowbase = (b * a.S + j0 + jl) * static_cast<long long>(a.n0);
+      if (a.n0 == P::N) store_any<LOGN, true>(v, a, kind, rowbase, 0.f, t);
+    }
+    return;
+  }
+
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const double s = a.scales[j0 + i];
     const cpx mp = morlet_params(s, a.dt, P::N);
