@@ -10,6 +10,7 @@ missing library raises.  The same functions are registered as torch custom ops
 from __future__ import annotations
 
 import ctypes as C
+import threading
 from typing import Optional, Sequence
 
 import numpy as np
@@ -55,12 +56,31 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+_F64_CACHE: "dict[tuple, torch.Tensor]" = {}
+_F64_CACHE_MAX = 256
+_F64_LOCK = threading.Lock()
+
+
 def _f64_dev(a, dev) -> Optional[torch.Tensor]:
+    """Host arrays (scale vectors, significance multipliers) as device float64 tensors.
+    A pageable host-to-device copy blocks the host until the stream drains, which
+    serialises back-to-back transforms; the copies are therefore content-addressed and
+    cached per device (the key is the array's bytes, so a changed array is a new entry)."""
     if a is None:
         return None
     if isinstance(a, torch.Tensor):
         return a.to(device=dev, dtype=torch.float64).contiguous()
-    return torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)
+    h = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    key = (str(dev), h.shape, h.tobytes())
+    with _F64_LOCK:
+        t = _F64_CACHE.get(key)
+    if t is None:
+        t = torch.as_tensor(h, device=dev)
+        with _F64_LOCK:
+            if len(_F64_CACHE) >= _F64_CACHE_MAX:
+                _F64_CACHE.pop(next(iter(_F64_CACHE)))
+            _F64_CACHE[key] = t
+    return t
 
 
 # ------------------------------------------------------------------------ moments
