@@ -158,6 +158,18 @@ __device__ __forceinline__ cpx smooth_band_bin(const cpx (&v)[16], cpx smt, int 
   return cscale(y, smt.y * __builtin_amdgcn_exp2f(smt.x * kk * kk));
 }
 
+// v[m] *= exp(-2 pi i K0 n / N) at n = t + m NT (K0 = N / 2^(4Q+1), a multiple of 16: one
+// phasor per thread): undoes the K0 shift of a smoothed row's band.
+template <int LOGN, int Q>
+__device__ __forceinline__ void band_phasor(cpx (&v)[16], int t) {
+  using P = FftPlan<LOGN>;
+  constexpr int K0 = P::N >> (4 * Q + 1);
+  asm volatile("" : "+v"(t));  // recompute per row: hoisted, the phasors spill (WCT VGPR budget 128)
+  const cpx ph = expi_frac(-K0 * t, P::N);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
+}
+
 // Smoothed row from its band bin: band exchange, inverse FFT from pass Q, time phasor
 // exp(-2 pi i K0 n / N) (K0 a multiple of 16: the same for the 16 positions of a thread).
 template <int LOGN, int Q, bool TWL, bool PHASOR = true>
@@ -173,13 +185,7 @@ __device__ __forceinline__ void smooth_from_band(cpx (&v)[16], cpx y, int slot, 
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = my[base + r * STEP];
   fft_row<LOGN, 1, 1, TWL, Q>(v, my, 0, tw, t, par, twl);
-  if constexpr (PHASOR) {
-    int tt = t;
-    asm volatile("" : "+v"(tt));  // recompute per row: hoisted, the phasors spill (WCT VGPR budget 128)
-    const cpx ph = expi_frac(-K0 * tt, P::N);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
-  }
+  if constexpr (PHASOR) band_phasor<LOGN, Q>(v, t);
 }
 
 // Inverse CWT row of phase A from the pair's spectrum row (global / L2), regime Q.

@@ -13,7 +13,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwtmi.so")
+# WTMI_LIB_PATH: load another build of the same ABI (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("WTMI_LIB_PATH") or os.path.join(_HERE, "libwtmi.so")
 
 _P = C.c_void_p
 _I64 = C.c_longlong
