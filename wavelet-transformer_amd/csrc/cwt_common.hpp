@@ -25,7 +25,8 @@ struct CwtArgs {
   float* out_v;
   int nchunks, chunk;
   int prune;             // allow band-pruned inverse transforms (band_regime); 0 = full FFTs
-  int diag;              // diagnostics only (WTMI_CWT_DIAG): 1 = skip the inverse FFTs, 2 = skip stores, 4 = stores only
+  int diag;              // diagnostics only (WTMI_CWT_DIAG): 1 = skip the inverse FFTs, 2 = skip stores,
+                         // 4 = stores only, 8 = start-up only (tables, load, forward FFT)
 };
 
 constexpr double kPi = 3.14159265358979323846;
