@@ -57,7 +57,8 @@ def test_cwt_rows_match_oracle(n0, dj, J):
                                             (8192, 1 / 24, 255, 0.0), (2000, 1 / 12, 110, 50.0)])
 def test_band_pruned_rows(n0, dj, J, offset, monkeypatch):
     """Rows whose filtered spectrum lies in bins [0, N/16^q) enter the inverse FFT at pass q
-    (cwt_common.hpp band_regime).  Random walks with a large mean put most of the energy at
+    (cwt_common.hpp band_regime); full-band rows run a first pass over their NZ non-zero
+    inputs only (first_pass_nz).  Random walks with a large mean put most of the energy at
     the lowest bins -- the worst case for the dropped negative-frequency tail."""
     rng = np.random.default_rng(n0 + 7)
     B = 2
@@ -69,12 +70,13 @@ def test_band_pruned_rows(n0, dj, J, offset, monkeypatch):
     xd = torch.tensor(x, device="cuda")
     monkeypatch.setenv("WTMI_CWT_PRUNE", "0")
     full = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
-    monkeypatch.setenv("WTMI_CWT_PRUNE", "1")
-    pr = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
-    assert row_relerr(pr.astype(np.complex128), full.astype(np.complex128)).max() < TOL
-    for b in range(B):
-        ref = pc.cwt(x[b].astype(np.float64), dt, dj, s0, J)[0]
-        assert row_relerr(pr[b].astype(np.complex128), ref).max() < TOL, b
+    for mode in ("1", "2"):  # band-pruned rows; + narrowed first passes of full-band rows
+        monkeypatch.setenv("WTMI_CWT_PRUNE", mode)
+        pr = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
+        assert row_relerr(pr.astype(np.complex128), full.astype(np.complex128)).max() < TOL, mode
+        for b in range(B):
+            ref = pc.cwt(x[b].astype(np.float64), dt, dj, s0, J)[0]
+            assert row_relerr(pr[b].astype(np.complex128), ref).max() < TOL, (mode, b)
 
 
 def test_many_scales_span_several_chunks():

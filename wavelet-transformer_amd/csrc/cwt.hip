@@ -103,6 +103,19 @@ __device__ __forceinline__ void inverse_row(cpx (&v)[16], const cpx (&X)[16], cp
       fft_row<LOGN, 1, NBUF, TWL, 1>(v, my, bufstride, tw, t, par, twl);
       return;
     }
+    if (q < 0) {  // full band, first pass narrowed: q = -log2(NZ)
+      if (q == -1) {
+        morlet_filter_nz<LOGN, 2>(v, X, prm, f0, t);
+        fft_row<LOGN, 1, NBUF, TWL, 0, 2>(v, my, bufstride, tw, t, par, twl);
+      } else if (q == -2) {
+        morlet_filter_nz<LOGN, 4>(v, X, prm, f0, t);
+        fft_row<LOGN, 1, NBUF, TWL, 0, 4>(v, my, bufstride, tw, t, par, twl);
+      } else {
+        morlet_filter_nz<LOGN, 8>(v, X, prm, f0, t);
+        fft_row<LOGN, 1, NBUF, TWL, 0, 8>(v, my, bufstride, tw, t, par, twl);
+      }
+      return;
+    }
   }
   morlet_filter<LOGN>(v, X, prm, f0, t);
   fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
@@ -146,7 +159,11 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
     const double s = a.scales[j0 + i];
     const cpx mp = morlet_params(s, a.dt, P::N);
     const float sg = a.sigscale ? static_cast<float>(a.sigscale[j0 + i]) : 0.f;
-    const int q = (a.prune && NBUF == 1) ? band_regime<LOGN>(s, a.dt, a.f0) : 0;
+    int q = (a.prune && NBUF == 1) ? band_regime<LOGN>(s, a.dt, a.f0) : 0;
+    if (q == 0 && a.prune >= 2 && NBUF == 1) {  // narrowed first pass
+      const int nz = first_pass_nz<LOGN>(s, a.dt, a.f0);
+      q = nz == 2 ? -1 : (nz == 4 ? -2 : (nz == 8 ? -3 : 0));
+    }
     prm_tab[i] = make_float4(mp.x, mp.y, sg, static_cast<float>(q));
   }
 
@@ -193,12 +210,17 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
     const cpx prm = mkc(prm4.x, prm4.y);
     // the iteration's band regime: the narrowest-band common to its rows (workgroup-uniform,
     // the transforms contain barriers)
-    int q = 3;
+    // codes by band width: 0 (full) > -3 (first pass 8 of 16) > -2 (4) > -1 (2) > 1 > 2
+    int rank = 6;
 #pragma unroll
     for (int gg = 0; gg < G::ROWS; ++gg) {
       const int jj = it * G::ROWS + gg;
-      if (jj < j1 - j0) q = min(q, static_cast<int>(prm_tab[jj].w));
+      if (jj < j1 - j0) {
+        const int qc = static_cast<int>(prm_tab[jj].w);
+        rank = min(rank, qc == 0 ? 0 : (qc < 0 ? 4 + qc : 3 + qc));
+      }
     }
+    const int q = rank == 0 ? 0 : (rank <= 3 ? rank - 4 : rank - 3);
     cpx v[16];
     if (a.diag & 1) {
 #pragma unroll
@@ -314,7 +336,8 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   nch = (a.S + chunk - 1) / chunk;
   a.nchunks = nch;
   a.chunk = chunk;
-  a.prune = env_int("WTMI_CWT_PRUNE", 1);
+  // 2: band-pruned rows and narrowed first passes; 1: band-pruned rows only; 0: full FFTs
+  a.prune = env_int("WTMI_CWT_PRUNE", 2);
   a.diag = env_int("WTMI_CWT_DIAG", 0);
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;

@@ -24,7 +24,8 @@ struct CwtArgs {
   float* out_u;
   float* out_v;
   int nchunks, chunk;
-  int prune;             // allow band-pruned inverse transforms (band_regime); 0 = full FFTs
+  int prune;             // 2: band-pruned rows (band_regime) + narrowed first passes (first_pass_nz);
+                         // 1: band-pruned rows only; 0: full FFTs
   int diag;              // diagnostics only (WTMI_CWT_DIAG): 1 = skip the inverse FFTs, 2 = skip stores,
                          // 4 = stores only, 8 = start-up only (tables, load, forward FFT)
 };
@@ -182,6 +183,38 @@ __device__ __forceinline__ int band_regime(double s, double dt, double f0) {
       q = qq;
   }
   return q;
+}
+
+// First-pass width of a full-band row: the smallest NZ in {2, 4, 8} such that the filtered
+// bins k = t + m NT with m >= NZ vanish (k >= NZ N/16: psi below exp(-kBandT^2/2) past the
+// edge; m >= 8 are the negative frequencies, dropped for f0 >= kBandF0); 16 otherwise.
+template <int LOGN>
+__device__ __forceinline__ int first_pass_nz(double s, double dt, double f0) {
+  using P = FftPlan<LOGN>;
+  if (f0 < kBandF0 || P::NT < 16) return 16;
+  const double alpha = s * 2.0 * kPi / (static_cast<double>(P::N) * dt);
+  if (alpha * static_cast<double>(2 * P::NT) - f0 >= kBandT) return 2;
+  if (alpha * static_cast<double>(4 * P::NT) - f0 >= kBandT) return 4;
+  return 8;
+}
+
+// v = X * psi_bar_j / N on the bins m < NZ (the rest zero, see first_pass_nz).
+template <int LOGN, int NZ>
+__device__ __forceinline__ void morlet_filter_nz(cpx (&v)[16], const cpx (&X)[16], cpx prm,
+                                                 float f0, int t) {
+  using P = FftPlan<LOGN>;
+  constexpr float K = -0.5f * kLog2e;
+  const float eb = fmaf(prm.x, static_cast<float>(t), -f0);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    if (m < NZ) {
+      const float off = static_cast<float>((m < 8 ? m : m - 16) * P::NT);
+      const float e = fmaf(prm.x, off, eb);
+      v[m] = cscale(X[m], __builtin_amdgcn_exp2f(fmaf(e * K, e, prm.y)));
+    } else {
+      v[m] = mkc(0.f, 0.f);
+    }
+  }
 }
 
 // Filtered bin t of a band-pruned row (thread t's m = 0 element, frequency index t >= 0).

@@ -119,6 +119,65 @@ __device__ __forceinline__ void dft16(cpx* v) {
     for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = t[4 * k1 + k2];
 }
 
+// dft4 with x2 = x3 = 0 (the two zero inputs fold away).
+template <int DIR>
+__device__ __forceinline__ void dft4_2(cpx& x0, cpx& x1, cpx& x2, cpx& x3) {
+  constexpr float sd = static_cast<float>(DIR);
+  const cpx a = x0, b = x1;
+  x0 = a + b;
+  x2 = a - b;
+  x1 = cfma(b.yx, cpx{-sd, sd}, a);
+  x3 = cfma(b.yx, cpx{sd, -sd}, a);
+}
+
+// 16-point DFT of v[0..15] whose inputs v[m] vanish for m >= NZ (NZ = 2, 4, 8; 16 = dft16):
+// the first radix-4 stage shrinks to two-input butterflies (NZ = 8) or copies (NZ <= 4), and
+// for NZ = 2 half of the twiddles and of the second stage's inputs are zero as well.
+template <int DIR, int NZ>
+__device__ __forceinline__ void dft16_nz(cpx* v) {
+  if constexpr (NZ >= 16) {
+    dft16<DIR>(v);
+  } else {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+      if constexpr (NZ == 8) {
+        dft4_2<DIR>(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]);
+      } else if (n2 < NZ) {
+        v[n2 + 4] = v[n2];
+        v[n2 + 8] = v[n2];
+        v[n2 + 12] = v[n2];
+      } else {
+        v[n2] = v[n2 + 4] = v[n2 + 8] = v[n2 + 12] = mkc(0.f, 0.f);
+      }
+    }
+    v[5] = rot16<DIR, 1>(v[5]);
+    v[9] = rot16<DIR, 2>(v[9]);
+    v[13] = rot16<DIR, 3>(v[13]);
+    if constexpr (NZ > 2) {
+      v[6] = rot16<DIR, 2>(v[6]);
+      v[10] = rot16<DIR, 4>(v[10]);
+      v[14] = rot16<DIR, 6>(v[14]);
+      v[7] = rot16<DIR, 3>(v[7]);
+      v[11] = rot16<DIR, 6>(v[11]);
+      v[15] = rot16<DIR, 9>(v[15]);
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      if constexpr (NZ > 2)
+        dft4<DIR>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+      else
+        dft4_2<DIR>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+    }
+    cpx t[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[i] = v[i];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = t[4 * k1 + k2];
+  }
+}
+
 template <int R, int DIR>
 __device__ __forceinline__ void dft_small(cpx* v) {
   if constexpr (R == 2) {
@@ -315,7 +374,7 @@ __device__ __forceinline__ void tail_butterflies(cpx* v, const cpx* b) {
 // START > 0 enters at radix-16 pass START with v[r] already holding that pass's
 // inputs (band-pruned inverse transforms, see band_entry below); the passes before
 // it are skipped.
-template <int LOGN, int DIR, int NBUF, bool TWL = false, int START = 0>
+template <int LOGN, int DIR, int NBUF, bool TWL = false, int START = 0, int NZ = 16>
 __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int bufstride,
                                         const cpx* tw, int t, int& par,
                                         const float4* twl = nullptr) {
@@ -323,7 +382,7 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
   static_assert(START == 0 || (START < P::P16 && NBUF == 1), "pruned entry: radix-16 pass, 1 buffer");
   constexpr bool kAligned = (P::NT % 32) == 0;  // strides are multiples of 32 -> pad is additive
   if constexpr (START == 0) {
-    dft16<DIR>(v);
+    dft16_nz<DIR, NZ>(v);  // NZ < 16: inputs v[m], m >= NZ, are zero (caller's guarantee)
     if constexpr (P::NPASS == 1) return;
     cpx* buf = lds + (NBUF == 2 ? par * bufstride : 0);
     if constexpr (NBUF == 1) __syncthreads();
