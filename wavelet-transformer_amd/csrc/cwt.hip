@@ -83,42 +83,53 @@ __device__ __forceinline__ void store_any(const cpx (&v)[16], const CwtArgs& a, 
 }
 
 // W row of one scale: Morlet filter + inverse FFT, entering the FFT at pass q when the
-// filtered spectrum is confined to bins [0, N/16^q) (band_regime / band_entry).
+// filtered spectrum is confined to bins [0, N/16^q) (band_regime / band_entry), with the
+// entry pass narrowed to its NZ non-zero inputs (row_code).
+template <int LOGN, int NBUF, bool TWL, int Q, int NZ>
+__device__ __forceinline__ void inverse_row_v(cpx (&v)[16], const cpx (&X)[16], cpx prm, float f0,
+                                              cpx* my, int bufstride, const cpx* tw, int t, int& par,
+                                              const float4* twl) {
+  if constexpr (Q == 0) {
+    if constexpr (NZ < 16)
+      morlet_filter_nz<LOGN, NZ>(v, X, prm, f0, t);
+    else
+      morlet_filter<LOGN>(v, X, prm, f0, t);
+    fft_row<LOGN, 1, NBUF, TWL, 0, NZ>(v, my, bufstride, tw, t, par, twl);
+  } else {
+    band_entry<LOGN, Q, NZ>(v, morlet_bin0(X[0], prm, f0, t), my, t);
+    fft_row<LOGN, 1, NBUF, TWL, Q, NZ>(v, my, bufstride, tw, t, par, twl);
+  }
+}
+
 template <int LOGN, int NBUF, bool TWL>
 __device__ __forceinline__ void inverse_row(cpx (&v)[16], const cpx (&X)[16], cpx prm, float f0,
-                                            int q, cpx* my, int bufstride, const cpx* tw, int t,
+                                            int code, cpx* my, int bufstride, const cpx* tw, int t,
                                             int& par, const float4* twl) {
   using P = FftPlan<LOGN>;
+#define WTMI_ROW(Q, NZ) inverse_row_v<LOGN, NBUF, TWL, Q, NZ>(v, X, prm, f0, my, bufstride, tw, t, par, twl)
   if constexpr (NBUF == 1 && P::P16 >= 2 && (P::NT % 16) == 0) {
-    if (q >= 1) {
-      const cpx y = morlet_bin0(X[0], prm, f0, t);
-      if constexpr (P::P16 >= 3 && (P::NT % 256) == 0) {
-        if (q >= 2) {
-          band_entry<LOGN, 2>(v, y, my, t);
-          fft_row<LOGN, 1, NBUF, TWL, 2>(v, my, bufstride, tw, t, par, twl);
-          return;
-        }
-      }
-      band_entry<LOGN, 1>(v, y, my, t);
-      fft_row<LOGN, 1, NBUF, TWL, 1>(v, my, bufstride, tw, t, par, twl);
-      return;
+    switch (code) {
+      case 1: WTMI_ROW(0, 8); return;
+      case 2: WTMI_ROW(0, 4); return;
+      case 3: WTMI_ROW(0, 2); return;
+      case 4: WTMI_ROW(1, 16); return;
+      case 5: WTMI_ROW(1, 8); return;
+      case 6: WTMI_ROW(1, 4); return;
+      case 7: WTMI_ROW(1, 2); return;
+      default: break;
     }
-    if (q < 0) {  // full band, first pass narrowed: q = -log2(NZ)
-      if (q == -1) {
-        morlet_filter_nz<LOGN, 2>(v, X, prm, f0, t);
-        fft_row<LOGN, 1, NBUF, TWL, 0, 2>(v, my, bufstride, tw, t, par, twl);
-      } else if (q == -2) {
-        morlet_filter_nz<LOGN, 4>(v, X, prm, f0, t);
-        fft_row<LOGN, 1, NBUF, TWL, 0, 4>(v, my, bufstride, tw, t, par, twl);
-      } else {
-        morlet_filter_nz<LOGN, 8>(v, X, prm, f0, t);
-        fft_row<LOGN, 1, NBUF, TWL, 0, 8>(v, my, bufstride, tw, t, par, twl);
+    if constexpr (P::P16 >= 3 && (P::NT % 256) == 0) {
+      switch (code) {
+        case 8: WTMI_ROW(2, 16); return;
+        case 9: WTMI_ROW(2, 8); return;
+        case 10: WTMI_ROW(2, 4); return;
+        case 11: WTMI_ROW(2, 2); return;
+        default: break;
       }
-      return;
     }
   }
-  morlet_filter<LOGN>(v, X, prm, f0, t);
-  fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
+  WTMI_ROW(0, 16);
+#undef WTMI_ROW
 }
 
 template <int LOGN, int NBUF, int MODE, int VAR = 0>
@@ -159,12 +170,8 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
     const double s = a.scales[j0 + i];
     const cpx mp = morlet_params(s, a.dt, P::N);
     const float sg = a.sigscale ? static_cast<float>(a.sigscale[j0 + i]) : 0.f;
-    int q = (a.prune && NBUF == 1) ? band_regime<LOGN>(s, a.dt, a.f0) : 0;
-    if (q == 0 && a.prune >= 2 && NBUF == 1) {  // narrowed first pass
-      const int nz = first_pass_nz<LOGN>(s, a.dt, a.f0);
-      q = nz == 2 ? -1 : (nz == 4 ? -2 : (nz == 8 ? -3 : 0));
-    }
-    prm_tab[i] = make_float4(mp.x, mp.y, sg, static_cast<float>(q));
+    const int code = NBUF == 1 ? row_code<LOGN>(s, a.dt, a.f0, a.prune) : 0;
+    prm_tab[i] = make_float4(mp.x, mp.y, sg, static_cast<float>(code));
   }
 
   constexpr bool TWL = G::TWL;
@@ -210,17 +217,14 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
     const cpx prm = mkc(prm4.x, prm4.y);
     // the iteration's band regime: the narrowest-band common to its rows (workgroup-uniform,
     // the transforms contain barriers)
-    // codes by band width: 0 (full) > -3 (first pass 8 of 16) > -2 (4) > -1 (2) > 1 > 2
-    int rank = 6;
+    // the iteration's row code: the widest band among its rows (workgroup-uniform, the
+    // transforms contain barriers)
+    int q = 12;
 #pragma unroll
     for (int gg = 0; gg < G::ROWS; ++gg) {
       const int jj = it * G::ROWS + gg;
-      if (jj < j1 - j0) {
-        const int qc = static_cast<int>(prm_tab[jj].w);
-        rank = min(rank, qc == 0 ? 0 : (qc < 0 ? 4 + qc : 3 + qc));
-      }
+      if (jj < j1 - j0) q = min(q, static_cast<int>(prm_tab[jj].w));
     }
-    const int q = rank == 0 ? 0 : (rank <= 3 ? rank - 4 : rank - 3);
     cpx v[16];
     if (a.diag & 1) {
 #pragma unroll

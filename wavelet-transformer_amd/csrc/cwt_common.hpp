@@ -24,7 +24,7 @@ struct CwtArgs {
   float* out_u;
   float* out_v;
   int nchunks, chunk;
-  int prune;             // 2: band-pruned rows (band_regime) + narrowed first passes (first_pass_nz);
+  int prune;             // 2: band-pruned rows + narrowed entry passes (row_code);
                          // 1: band-pruned rows only; 0: full FFTs
   int diag;              // diagnostics only (WTMI_CWT_DIAG): 1 = skip the inverse FFTs, 2 = skip stores,
                          // 4 = stores only, 8 = start-up only (tables, load, forward FFT)
@@ -185,20 +185,27 @@ __device__ __forceinline__ int band_regime(double s, double dt, double f0) {
   return q;
 }
 
-// First-pass width of a full-band row: the smallest NZ in {2, 4, 8} such that the filtered
-// bins k = t + m NT with m >= NZ vanish (k >= NZ N/16: psi below exp(-kBandT^2/2) past the
-// edge; m >= 8 are the negative frequencies, dropped for f0 >= kBandF0); 16 otherwise.
+// Row code (0..11) = 4 q + k: band regime q (band_regime) and width NZ = 16 >> k of the
+// transform's entry pass -- its inputs r >= NZ vanish.  Entry pass q reads bins
+// (t >> 4q) + r (NT >> 4q) (q >= 1) or t + r NT (q = 0), so r >= NZ means bins >= NZ * unit:
+// narrowed when psi is below exp(-kBandT^2/2) there; for q = 0, r >= 8 are the negative
+// frequencies (dropped for f0 >= kBandF0), so NZ <= 8 always.  A smaller code is a wider band:
+// the rows of one iteration run at their smallest code.
 template <int LOGN>
-__device__ __forceinline__ int first_pass_nz(double s, double dt, double f0) {
+__device__ __forceinline__ int row_code(double s, double dt, double f0, int prune) {
   using P = FftPlan<LOGN>;
-  if (f0 < kBandF0 || P::NT < 16) return 16;
+  if (!prune) return 0;
+  const int q = band_regime<LOGN>(s, dt, f0);
+  if (prune < 2 || f0 < kBandF0 || P::NT < 16) return 4 * q;
   const double alpha = s * 2.0 * kPi / (static_cast<double>(P::N) * dt);
-  if (alpha * static_cast<double>(2 * P::NT) - f0 >= kBandT) return 2;
-  if (alpha * static_cast<double>(4 * P::NT) - f0 >= kBandT) return 4;
-  return 8;
+  const double unit = static_cast<double>(q == 0 ? P::NT : (P::NT >> (4 * q)));
+  int k = q == 0 ? 1 : 0;  // NZ = 8 / 16
+  if (alpha * 4.0 * unit - f0 >= kBandT) k = 2;  // NZ = 4
+  if (alpha * 2.0 * unit - f0 >= kBandT) k = 3;  // NZ = 2
+  return 4 * q + k;
 }
 
-// v = X * psi_bar_j / N on the bins m < NZ (the rest zero, see first_pass_nz).
+// v = X * psi_bar_j / N on the bins m < NZ (the rest zero, see row_code).
 template <int LOGN, int NZ>
 __device__ __forceinline__ void morlet_filter_nz(cpx (&v)[16], const cpx (&X)[16], cpx prm,
                                                  float f0, int t) {

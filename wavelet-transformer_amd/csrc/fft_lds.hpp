@@ -289,44 +289,57 @@ __device__ __forceinline__ cpx opaque(cpx w) {
   return w;
 }
 
-// v[r] *= w^r for r = 1..15 from the bases w, w^2, w^4, w^8.
-template <int DIR>
-__device__ __forceinline__ void apply_tw16_w(cpx* v, cpx w1, cpx w2, cpx w4, cpx w8) {
+// v[r] *= w^r for r = 1..NZ-1 from the bases w, w^2, w^4, w^8 (inputs r >= NZ are zero
+// and stay untouched; NZ = 16: all 15).
+template <int DIR, int NZ>
+__device__ __forceinline__ void apply_tw16_w_nz(cpx* v, cpx w1, cpx w2, cpx w4, cpx w8) {
   w1 = twd<DIR>(w1);
-  w2 = twd<DIR>(w2);
-  w4 = twd<DIR>(w4);
-  w8 = twd<DIR>(w8);
-  const cpx w3 = cmul(w1, w2), w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
+  if constexpr (NZ > 2) {
+    w2 = twd<DIR>(w2);
+    const cpx w3 = cmul(w1, w2);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], w3);
+    if constexpr (NZ > 4) {
+      w4 = twd<DIR>(w4);
+      const cpx w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
+      v[4] = cmul(v[4], w4);
+      v[5] = cmul(v[5], w5);
+      v[6] = cmul(v[6], w6);
+      v[7] = cmul(v[7], w7);
+      if constexpr (NZ > 8) {
+        w8 = twd<DIR>(w8);
+        v[8] = cmul(v[8], w8);
+        v[9] = cmul(v[9], cmul(w8, w1));
+        v[10] = cmul(v[10], cmul(w8, w2));
+        v[11] = cmul(v[11], cmul(w8, w3));
+        v[12] = cmul(v[12], cmul(w8, w4));
+        v[13] = cmul(v[13], cmul(w8, w5));
+        v[14] = cmul(v[14], cmul(w8, w6));
+        v[15] = cmul(v[15], cmul(w8, w7));
+      }
+    }
+  }
   v[1] = cmul(v[1], w1);
-  v[2] = cmul(v[2], w2);
-  v[3] = cmul(v[3], w3);
-  v[4] = cmul(v[4], w4);
-  v[5] = cmul(v[5], w5);
-  v[6] = cmul(v[6], w6);
-  v[7] = cmul(v[7], w7);
-  v[8] = cmul(v[8], w8);
-  v[9] = cmul(v[9], cmul(w8, w1));
-  v[10] = cmul(v[10], cmul(w8, w2));
-  v[11] = cmul(v[11], cmul(w8, w3));
-  v[12] = cmul(v[12], cmul(w8, w4));
-  v[13] = cmul(v[13], cmul(w8, w5));
-  v[14] = cmul(v[14], cmul(w8, w6));
-  v[15] = cmul(v[15], cmul(w8, w7));
 }
 
 template <int DIR>
+__device__ __forceinline__ void apply_tw16_w(cpx* v, cpx w1, cpx w2, cpx w4, cpx w8) {
+  apply_tw16_w_nz<DIR, 16>(v, w1, w2, w4, w8);
+}
+
+template <int DIR, int NZ = 16>
 __device__ __forceinline__ void apply_tw16(cpx* v, const cpx* b) {
-  apply_tw16_w<DIR>(v, opaque(b[0]), opaque(b[1]), opaque(b[2]), opaque(b[3]));
+  apply_tw16_w_nz<DIR, NZ>(v, opaque(b[0]), opaque(b[1]), opaque(b[2]), opaque(b[3]));
 }
 
 // Same from the LDS table: entry k of pass p.  The asm barrier keeps the two reads
 // inside the caller's loop (their LDS region is never written, so LICM would
 // otherwise hoist them and keep the 8 values live in registers).
-template <int DIR, int E>
+template <int DIR, int E, int NZ = 16>
 __device__ __forceinline__ void apply_tw16_lds(cpx* v, const float4* tab, int idx) {
   asm volatile("" : "+v"(idx));
   const float4 a = tab[idx], b = tab[E + idx];
-  apply_tw16_w<DIR>(v, mkc(a.x, a.y), mkc(a.z, a.w), mkc(b.x, b.y), mkc(b.z, b.w));
+  apply_tw16_w_nz<DIR, NZ>(v, mkc(a.x, a.y), mkc(a.z, a.w), mkc(b.x, b.y), mkc(b.z, b.w));
 }
 
 // Trailing radix-R pass, butterfly Q: v[r] *= (w_t * exp(2 pi i Q/16))^r, r = 1..R-1, from
@@ -409,11 +422,19 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
         }
         if constexpr (NBUF == 2) par ^= 1;
       }
-      if constexpr (TWL)
-        apply_tw16_lds<DIR, P::TWL_E>(v, twl, twl_base(p) + (t & (ns - 1)));
-      else
-        apply_tw16<DIR>(v, tw + 4 * (p - 1));
-      dft16<DIR>(v);
+      if (START > 0 && p == START) {  // entry pass of a pruned row: inputs r >= NZ are zero
+        if constexpr (TWL)
+          apply_tw16_lds<DIR, P::TWL_E, NZ>(v, twl, twl_base(p) + (t & (ns - 1)));
+        else
+          apply_tw16<DIR, NZ>(v, tw + 4 * (p - 1));
+        dft16_nz<DIR, NZ>(v);
+      } else {
+        if constexpr (TWL)
+          apply_tw16_lds<DIR, P::TWL_E>(v, twl, twl_base(p) + (t & (ns - 1)));
+        else
+          apply_tw16<DIR>(v, tw + 4 * (p - 1));
+        dft16<DIR>(v);
+      }
       if (!last) {
         cpx* wbuf = lds + (NBUF == 2 ? par * bufstride : 0);
         const int idxD = (t / ns) * ns * 16 + (t & (ns - 1));
@@ -469,7 +490,7 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
 // bin t (its m = 0 element) in y; bins are exchanged through lds[0 .. N/16^Q) (one b64 write
 // per thread, 16 broadcast reads), and fft_row<..., START = Q> takes it from there.
 // Saves Q radix-16 passes (butterflies, twiddles, Q-1 LDS exchanges, 15/16 of one).
-template <int LOGN, int Q>
+template <int LOGN, int Q, int NZ = 16>
 __device__ __forceinline__ void band_entry(cpx (&v)[16], cpx y, cpx* __restrict__ lds, int t) {
   using P = FftPlan<LOGN>;
   static_assert(Q >= 1 && Q < P::P16 && (P::NT % (1 << (4 * Q))) == 0, "band entry");
@@ -480,7 +501,7 @@ __device__ __forceinline__ void band_entry(cpx (&v)[16], cpx y, cpx* __restrict_
   __syncthreads();
   const int base = t >> (4 * Q);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = lds[base + r * STEP];
+  for (int r = 0; r < 16; ++r) v[r] = r < NZ ? lds[base + r * STEP] : mkc(0.f, 0.f);
 }
 
 }  // namespace wtmi
