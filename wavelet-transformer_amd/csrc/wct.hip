@@ -545,25 +545,49 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
   const int last = plan[S];
   if (last < 0) return;
   const int jend = last + HI + 1;  // output rows i = j - HI <= last
+  const int jlim = min(S, jend);   // rows read
+  // Rows are loaded D ahead of their use (D | K, so the pending slot of row jb + r is r % D):
+  // D rows of loads in flight per thread instead of one.
+  constexpr int D = (K % 6 == 0) ? 6 : (K % 5 == 0) ? 5 : (K % 4 == 0) ? 4 : (K % 3 == 0) ? 3 : (K % 2 == 0) ? 2 : 1;
+  V pa[D], pc[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (d < jlim) {
+      pa[d] = cola[static_cast<long long>(d) * ldv];
+      pc[d] = colb[static_cast<long long>(d) * ldv];
+    }
+  }
   for (int jb = 0; jb < jend; jb += K) {
+    int fl[K];  // the block's output-row plan flags, loaded up front (uniform scalar loads)
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int i = jb + r - HI;
+      fl[r] = (i >= 0 && i < S) ? plan[i] : kPlanSpec;
+    }
 #pragma unroll
     for (int r = 0; r < K; ++r) {
       const int j = jb + r;
-      if (j < S) {
-        const V a = cola[static_cast<long long>(j) * ldv], c = colb[static_cast<long long>(j) * ldv];
-        const float* pa = reinterpret_cast<const float*>(&a);
-        const float* pc = reinterpret_cast<const float*>(&c);
+      const int slot = r % D;
+      if (j < jlim) {
+        const V a = pa[slot], c = pc[slot];
+        const float* pap = reinterpret_cast<const float*>(&a);
+        const float* pcp = reinterpret_cast<const float*>(&c);
 #pragma unroll
         for (int f = 0; f < F; ++f) {
-          ra[r][f] = pa[f];
-          rb[r][f] = pc[f];
+          ra[r][f] = pap[f];
+          rb[r][f] = pcp[f];
+        }
+        const int jn = j + D;
+        if (jn < jlim) {
+          pa[slot] = cola[static_cast<long long>(jn) * ldv];
+          pc[slot] = colb[static_cast<long long>(jn) * ldv];
         }
       } else {
 #pragma unroll
         for (int f = 0; f < F; ++f) ra[r][f] = rb[r][f] = 0.f;
       }
       const int i = j - HI;
-      if (i >= 0 && i < S && !(plan[i] & kPlanSpec)) {
+      if (i >= 0 && i < S && !(fl[r] & kPlanSpec)) {
         float acc[2][F] = {};
 #pragma unroll
         for (int q = 0; q < K; ++q) {
@@ -751,7 +775,10 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int*
 template <int K>
 static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0, int S, float* coh,
                           const int* plan, hipStream_t st) {
-  const bool pairs = (n0 % 2) == 0;  // 16-byte column pairs need even rows
+  // one column per thread by default (twice the threads, more loads in flight: C4 4.73 ->
+  // 4.65 ms); WTMI_WCT_B_COLS=2: 16-byte column pairs (even rows)
+  const char* ec = getenv("WTMI_WCT_B_COLS");
+  const bool pairs = (n0 % 2) == 0 && ec && atoi(ec) == 2;
   const long long ncol = pairs ? n0 / 2 : n0;
   const long long tiles = (ncol + 255) / 256;
   const long long grid = batch * tiles;
