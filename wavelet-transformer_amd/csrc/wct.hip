@@ -80,22 +80,28 @@ __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, c
   for (int m = 0; m < 16; ++m) o[t + m * P::NT] = X[m];
 }
 
-// The spectra are loop-invariant: an opaque pointer stops the compiler from hoisting
-// the 2 x 16 loads out of the scale loop (which costs 64 VGPRs and spills).
-template <int LOGN>
-__device__ __forceinline__ void load_spec(cpx (&X)[16], const cpx* row, int t) {
+// Bins m < NZ of the pair's spectrum row (the rest are not read; see row_code).  The
+// spectra are loop-invariant: an opaque pointer stops the compiler from hoisting the
+// 2 x 16 loads out of the scale loop (which costs 64 VGPRs and spills).
+template <int LOGN, int NZ>
+__device__ __forceinline__ void load_spec_nz(cpx (&X)[16], const cpx* row, int t) {
   using P = FftPlan<LOGN>;
   if constexpr (P::NT >= kWave) {
     const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row);
     int voff = 8 * t;
     asm volatile("" : "+v"(voff));
 #pragma unroll
-    for (int m = 0; m < 16; ++m) X[m] = buf_ld_c64(r, voff, 8 * m * P::NT);
+    for (int m = 0; m < 16; ++m) X[m] = m < NZ ? buf_ld_c64(r, voff, 8 * m * P::NT) : mkc(0.f, 0.f);
   } else {
     asm volatile("" : "+s"(row));
 #pragma unroll
-    for (int m = 0; m < 16; ++m) X[m] = row[t + m * P::NT];
+    for (int m = 0; m < 16; ++m) X[m] = m < NZ ? row[t + m * P::NT] : mkc(0.f, 0.f);
   }
+}
+
+template <int LOGN>
+__device__ __forceinline__ void load_spec(cpx (&X)[16], const cpx* row, int t) {
+  load_spec_nz<LOGN, 16>(X, row, t);
 }
 
 // Row store of 16 positions per thread.  BUF (full rows owned by whole waves): buffer
@@ -189,7 +195,7 @@ __device__ __forceinline__ void smooth_from_band(cpx (&v)[16], cpx y, int slot, 
 }
 
 // Inverse CWT row of phase A from the pair's spectrum row (global / L2), regime Q.
-template <int LOGN, int Q, bool TWL>
+template <int LOGN, int Q, bool TWL, int NZ = 16>
 __device__ __forceinline__ void wct_inverse_row(cpx (&v)[16], const cpx* spec_row, cpx prm, float f0,
                                                 cpx* my, const cpx* tw, int t, int& par,
                                                 const float4* twl) {
@@ -197,10 +203,13 @@ __device__ __forceinline__ void wct_inverse_row(cpx (&v)[16], const cpx* spec_ro
     asm volatile("" : "+s"(spec_row));  // keep the one load inside the scale loop
     band_entry<LOGN, Q>(v, morlet_bin0(spec_row[t], prm, f0, t), my, t);
     fft_row<LOGN, 1, 1, TWL, Q>(v, my, 0, tw, t, par, twl);
-  } else {
-    load_spec<LOGN>(v, spec_row, t);
-    morlet_filter<LOGN>(v, v, prm, f0, t);
-    fft_row<LOGN, 1, 1, TWL>(v, my, 0, tw, t, par, twl);
+  } else {  // full band; NZ = 8: the negative-frequency half is negligible (f0 >= kBandF0)
+    load_spec_nz<LOGN, NZ>(v, spec_row, t);
+    if constexpr (NZ < 16)
+      morlet_filter_nz<LOGN, NZ>(v, v, prm, f0, t);
+    else
+      morlet_filter<LOGN>(v, v, prm, f0, t);
+    fft_row<LOGN, 1, 1, TWL, 0, NZ>(v, my, 0, tw, t, par, twl);
   }
 }
 
@@ -299,7 +308,7 @@ struct WctRowCtx {
 //   Q = 0: W1, W2 -> z1 = |W1|^2 + i |W2|^2, W12 -> full smoothing transforms of both.
 //   Q >= 1: pruned inverse transforms, and once each forward transform is done only the one
 //   band bin per thread is kept (2 VGPRs), so W12's outputs and transforms run with z1 dead.
-template <int LOGN, bool FULL, int Q, bool TWL>
+template <int LOGN, bool FULL, int Q, bool TWL, int NZ = 16>
 __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, int r0, int r1, cpx* my,
                                          const cpx* tw, int g, int t, int& par, const float4* twl) {
   using P = FftPlan<LOGN>;
@@ -374,10 +383,10 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       }
       continue;
     }
-    wct_inverse_row<LOGN, Q, TWL>(v, c.spec1, prm, f0, my, tw, t, par, twl);
+    wct_inverse_row<LOGN, Q, TWL, NZ>(v, c.spec1, prm, f0, my, tw, t, par, twl);
 #pragma unroll
     for (int m = 0; m < 16; ++m) w1[m] = v[m];
-    wct_inverse_row<LOGN, Q, TWL>(v, c.spec2, prm, f0, my, tw, t, par, twl);
+    wct_inverse_row<LOGN, Q, TWL, NZ>(v, c.spec2, prm, f0, my, tw, t, par, twl);
     // W12 = W1 conj(W2), z1 = |W1|^2 + i |W2|^2, zero past n0 (the reference smooths the
     // row zero-padded to N)
 #pragma unroll
@@ -491,7 +500,10 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     int r1 = r0 + 1;
     while (r1 < nrow && q_tab[r1] == q) ++r1;
     if (q == 0) {
-      wct_rows<LOGN, FULL, 0, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);
+      if (a.prune && a.f0 >= kBandF0 && P::NT >= 16)  // negative frequencies dropped: half the bins
+        wct_rows<LOGN, FULL, 0, TWL, 8>(a, c, r0, r1, my, tw, g, t, par, twl);
+      else
+        wct_rows<LOGN, FULL, 0, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);
     } else {
       if constexpr (P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
         if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
