@@ -27,6 +27,26 @@ struct FilterBank {
 
 __device__ __forceinline__ int wrap(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
+// 2^(j-1) mod n without a 64-bit division while 2^(j-1) < n (every level of n >= 2^J).
+__device__ __forceinline__ int dilation_mod(int j, int n) {
+  if (j <= 31) {
+    const unsigned p = 1u << (j - 1);
+    if (p < static_cast<unsigned>(n)) return static_cast<int>(p);
+  }
+  return static_cast<int>((1ll << (j - 1)) % n);
+}
+
+// Scalar tap offsets (dq * l) mod ng, l = 0..L-1, by repeated addition (dq < ng).
+template <int L>
+__device__ __forceinline__ void tap_offsets(int dq, int ng, int (&off)[L]) {
+  off[0] = 0;
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    const int o = off[l - 1] + dq;
+    off[l] = o >= ng ? o - ng : o;
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // analysis
 template <int LT>
@@ -286,20 +306,20 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
   for (int q = tid; q < ng; q += T) V4[q] = xin[q];
   __syncthreads();
   for (int j = 1; j <= level; ++j) {
-    const int dm = static_cast<int>((1ll << (j - 1)) % n);
+    const int dm = dilation_mod(j, n);
     float4* wrow = reinterpret_cast<float4*>(wout + static_cast<long long>(j - 1) * n);
     int tl = tid;
     asm volatile("" : "+v"(tl));
     float4 vreg[GROUPS];
     if (CHAIN && (dm & 3) == 0 && GROUPS * T == ng) {
       const int dq = dm >> 2;
-      if ((dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) {
+      if ((dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0 && (ng & (ng - 1)) == 0) {
         const int dqlog = __builtin_ctz(dq);
         const int q0 = (tl >> dqlog) * GROUPS * dq + (tl & (dq - 1));
         float4 vv[GROUPS + L - 1];  // chain elements q0 + (k - L + 1) dq
 #pragma unroll
         for (int k = 0; k < GROUPS + L - 1; ++k)
-          vv[k] = V4[(q0 + (k - (L - 1)) * dq + (L - 1) * ng) % ng];
+          vv[k] = V4[(q0 + (k - (L - 1)) * dq + (L - 1) * ng) & (GROUPS * T - 1)];  // ng = GROUPS*T
 #pragma unroll
         for (int m = 0; m < GROUPS; ++m) {
           float4 aw = make_float4(0.f, 0.f, 0.f, 0.f), av = aw;
@@ -330,10 +350,11 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
       } else {
         aw = make_float4(0.f, 0.f, 0.f, 0.f);
         av = aw;
-        const int dq = dm >> 2;
+        int off[L];
+        tap_offsets<L>(dm >> 2, ng, off);
 #pragma unroll
         for (int l = 0; l < L; ++l) {
-          int qs = q - (dq * l) % ng;
+          int qs = q - off[l];
           if (qs < 0) qs += ng;
           const float4 s = V4[qs];
           fma4(aw, fb.h[l], s);
@@ -383,7 +404,8 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
       pin4(vreg[k]);
     }
   } else {
-    const int dq = dm >> 2;
+    int off[L];
+    tap_offsets<L>(dm >> 2, ng, off);
 #pragma unroll
     for (int k = 0; k < GROUPS; ++k) {
       int q = min(tid + k * T, ng - 1);
@@ -391,7 +413,7 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
       float4 acc = z4;
 #pragma unroll
       for (int l = 0; l < L; ++l) {
-        int qs = q + (dq * l) % ng;
+        int qs = q + off[l];
         if (qs >= ng) qs -= ng;
         fma4(acc, fb.g[l], V4[PAD ? vpad(qs) : qs]);
         fma4(acc, wsel * fb.h[l], W4[qs]);
@@ -408,19 +430,21 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
 // (global) and of V_j (LDS) once and slides over them -- (M+L-1)/M loads per output
 // instead of L (the 8x re-read of W_j through L2 is what bounds the stride-T form).
 // Lanes with consecutive r read consecutive groups: coalesced for dq >= 64 groups,
-// dq-group contiguous runs below that.  Needs ng == M*T and ng % (M*dq) == 0.
-template <int L, int M, bool PAD = false>
+// dq-group contiguous runs below that.  NG = M*T groups, a power of two (the wrap is a
+// mask: a per-lane '% ng' was ~30 % of the kernel's VALU instructions); NG % (M*dq) == 0.
+template <int L, int M, int NG, bool PAD = false>
 __device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, const float4* __restrict__ W4,
-                                               int ng, int dqlog, const float (&hs)[L],
+                                               int dqlog, const float (&hs)[L],
                                                const FilterBank& fb, int tid, float4 (&vreg)[M]) {
+  static_assert((NG & (NG - 1)) == 0, "chain levels need a power-of-two group count");
   const int dq = 1 << dqlog;
   const int q0 = (tid >> dqlog) * M * dq + (tid & (dq - 1));
   float4 wv[M + L - 1], vv[M + L - 1];
 #pragma unroll
-  for (int k = 0; k < M + L - 1; ++k) wv[k] = W4[(q0 + k * dq) % ng];  // taps may wrap >1x
+  for (int k = 0; k < M + L - 1; ++k) wv[k] = W4[(q0 + k * dq) & (NG - 1)];  // taps may wrap >1x
 #pragma unroll
   for (int k = 0; k < M + L - 1; ++k) {
-    const int qv = (q0 + k * dq) % ng;
+    const int qv = (q0 + k * dq) & (NG - 1);
     vv[k] = V4[PAD ? vpad(qv) : qv];
   }
 #pragma unroll
@@ -483,12 +507,13 @@ __global__ void __launch_bounds__(T)
       for (int k = 0; k < GROUPS; ++k) pre[k] = wn[min(tid + k * T, ng - 1)];
     }
     const float wsel = ((keep >> (j - 1)) & 1ull) ? 1.f : 0.f;  // masked rows count as 0
-    const int dm = static_cast<int>((1ll << (j - 1)) % n);
+    const int dm = dilation_mod(j, n);
     int tl = tid;
     asm volatile("" : "+v"(tl));  // per-level copy: keeps address math out of LICM
     float4 vreg[GROUPS];
     int dqlog = -1;
-    if (MODE == 3 && (dm & 3) == 0 && GROUPS * T == ng) {
+    constexpr int NG = GROUPS * T;
+    if (MODE == 3 && (dm & 3) == 0 && NG == ng && (NG & (NG - 1)) == 0) {
       const int dq = dm >> 2;
       if ((dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) dqlog = __builtin_ctz(dq);
     }
@@ -496,7 +521,7 @@ __global__ void __launch_bounds__(T)
       float hs[L];
 #pragma unroll
       for (int l = 0; l < L; ++l) hs[l] = wsel * fb.h[l];
-      const int q0 = syn_level_chain<L, GROUPS, PAD>(V4, wr, ng, dqlog, hs, fb, tl, vreg);
+      const int q0 = syn_level_chain<L, GROUPS, (NG & (NG - 1)) == 0 ? NG : 1, PAD>(V4, wr, dqlog, hs, fb, tl, vreg);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < GROUPS; ++k) V4[vp(q0 + (k << dqlog))] = vreg[k];
