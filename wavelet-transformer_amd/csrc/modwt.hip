@@ -289,11 +289,11 @@ __device__ __forceinline__ void fma4(float4& acc, float c, const float4& s) {
 // result before the barrier; without both, the compiler hoists per-group address math
 // out of the level loop and sinks the tap FMAs past the barrier, keeping every LDS
 // operand live (256 VGPRs + spills).
-// CHAIN: levels with a whole-group dilation use the dilation-chain mapping of
-// syn_level_chain (taps m-L+1 .. m of the thread's chain, M+L-1 LDS reads for M
-// outputs instead of L*M); W_j stores then run along the chain (coalesced for
-// dq >= 64 groups, dq-group runs below).
-template <int L, int GROUPS, int T, bool CHAIN = false>
+// CHAIN > 0: levels with a dilation of dq >= CHAIN whole groups use the dilation-chain
+// mapping of syn_level_chain (taps m-L+1 .. m of the thread's chain, M+L-1 LDS reads for
+// M outputs instead of L*M); W_j stores then run along the chain (coalesced for
+// dq >= 64 groups, dq-group runs below: whole 128-byte lines from dq = 8).
+template <int L, int GROUPS, int T, int CHAIN = 0>
 __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ x, long long ld,
                                                       int n, int level, FilterBank fb,
                                                       float* __restrict__ w) {
@@ -311,9 +311,9 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
     int tl = tid;
     asm volatile("" : "+v"(tl));
     float4 vreg[GROUPS];
-    if (CHAIN && (dm & 3) == 0 && GROUPS * T == ng) {
+    if (CHAIN > 0 && (dm & 3) == 0 && GROUPS * T == ng) {
       const int dq = dm >> 2;
-      if ((dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0 && (ng & (ng - 1)) == 0) {
+      if (dq >= CHAIN && (dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0 && (ng & (ng - 1)) == 0) {
         const int dqlog = __builtin_ctz(dq);
         const int q0 = (tl >> dqlog) * GROUPS * dq + (tl & (dq - 1));
         float4 vv[GROUPS + L - 1];  // chain elements q0 + (k - L + 1) dq
@@ -602,7 +602,11 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
     else if (var == 1)
       launch(modwt_vec_kernel<8, 4, 1024>, 1024);
     else if (var == 2)
-      launch(modwt_vec_kernel<8, 8, 512, true>, 512);
+      launch(modwt_vec_kernel<8, 8, 512, 1>, 512);
+    else if (var == 5)
+      launch(modwt_vec_kernel<8, 8, 512, 8>, 512);
+    else if (var == 6)
+      launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
     else
       launch(modwt_vec_kernel<8, 8, 512>, 512);  // C3 A/B: 1.62 vs 1.65 ms
   } else if (n_taps == 8) {
