@@ -97,6 +97,21 @@ def test_modwt_batched_round_trip_and_energy(n, db4):
         _check_rows(wn[b], ref)
 
 
+@pytest.mark.parametrize("n,J", [(64, 9), (200, 10), (1000, 12), (4096, 13)])
+def test_modwt_dilations_past_n(n, J, db4):
+    """Levels whose dilation 2^(j-1) reaches or passes n (taken mod n, possibly 0):
+    the vectorised kernels' dilation/tap-offset arithmetic vs the textbook oracle."""
+    rng = np.random.default_rng(n + J)
+    x = np.stack([red_series(rng, n) for _ in range(3)])
+    ops = _ops()
+    w = ops.modwt(torch.tensor(x, device="cuda"), db4["dec_lo"], db4["dec_hi"], J)
+    wn = w.cpu().numpy()
+    for b in range(3):
+        _check_rows(wn[b], ms.modwt_direct(x[b].astype(np.float64), db4["dec_lo"], db4["dec_hi"], J))
+    xr = ops.imodwt(w, db4["dec_lo"], db4["dec_hi"]).cpu().numpy()
+    assert np.abs(xr - x).max() <= TOL * np.abs(x).max()
+
+
 def test_modwt_other_filter_lengths(pywt_filters):
     rng = np.random.default_rng(3)
     ops = _ops()

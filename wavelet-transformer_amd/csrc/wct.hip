@@ -658,13 +658,28 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
     const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
     cpx yz = mkc(0.f, 0.f), yw = mkc(0.f, 0.f);
     if (holder) {
-      for (int q = 0; q < K; ++q) {
-        const int rr = i - LO + q;
-        if (rr < 0 || rr >= a.S) continue;
-        const float w = (K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn;
-        const cpx* sb = SB + (b * a.S + rr) * 2ll * P::NT;
-        yz = cfma(cpx{w, w}, sb[tt], yz);
-        yw = cfma(cpx{w, w}, sb[P::NT + tt], yw);
+      // window rows in groups of U with every load of a group issued before its first
+      // use (one memory latency per group, not per row); rows outside [0, S) get weight 0
+      constexpr int U = 4;
+      const cpx* sbb = SB + b * a.S * 2ll * P::NT + tt;
+      for (int q0 = 0; q0 < K; q0 += U) {
+        cpx lz[U], lw[U];
+        float wq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int q = q0 + u;
+          const int rr = i - LO + q;
+          const bool ok = q < K && rr >= 0 && rr < a.S;
+          wq[u] = ok ? ((K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn) : 0.f;
+          const cpx* sb = sbb + (ok ? rr : i) * 2ll * P::NT;
+          lz[u] = sb[0];
+          lw[u] = sb[P::NT];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          yz = cfma(cpx{wq[u], wq[u]}, lz[u], yz);
+          yw = cfma(cpx{wq[u], wq[u]}, lw[u], yw);
+        }
       }
     }
     const int slot = holder ? k + K0 : -1;
