@@ -606,9 +606,9 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
     else if (var == 5)
       launch(modwt_vec_kernel<8, 8, 512, 8>, 512);
     else if (var == 6)
+      launch(modwt_vec_kernel<8, 8, 512>, 512);  // stride form for every level
+    else  // one-process A/B on two boxes (ms): stride 1.248 / 1.264, chains from dq 8 1.200 / 1.264, from dq 16 1.200 / 1.267
       launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
-    else
-      launch(modwt_vec_kernel<8, 8, 512>, 512);  // C3 A/B: 1.62 vs 1.65 ms
   } else if (n_taps == 8) {
     allow_lds(modwt_kernel<8>, lds);
     hipLaunchKernelGGL(modwt_kernel<8>, dim3(batch), dim3(block), lds, st, x, ld, ni, level, n_taps, fb, w);
