@@ -432,16 +432,27 @@ __device__ __forceinline__ void syn_level(const float4* __restrict__ V4, const f
 // Lanes with consecutive r read consecutive groups: coalesced for dq >= 64 groups,
 // dq-group contiguous runs below that.  NG = M*T groups, a power of two (the wrap is a
 // mask: a per-lane '% ng' was ~30 % of the kernel's VALU instructions); NG % (M*dq) == 0.
-template <int L, int M, int NG, bool PAD = false>
-__device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, const float4* __restrict__ W4,
-                                               int dqlog, const float (&hs)[L],
-                                               const FilterBank& fb, int tid, float4 (&vreg)[M]) {
-  static_assert((NG & (NG - 1)) == 0, "chain levels need a power-of-two group count");
+template <int M>
+__device__ __forceinline__ int chain_q0(int tid, int dqlog) {
+  return (tid >> dqlog) * M * (1 << dqlog) + (tid & ((1 << dqlog) - 1));
+}
+
+template <int L, int M, int NG, int K0 = 0, int K1 = M + L - 1>
+__device__ __forceinline__ void chain_load_w(const float4* __restrict__ W4, int dqlog, int tid,
+                                             float4 (&wv)[M + L - 1]) {
   const int dq = 1 << dqlog;
-  const int q0 = (tid >> dqlog) * M * dq + (tid & (dq - 1));
-  float4 wv[M + L - 1], vv[M + L - 1];
+  const int q0 = chain_q0<M>(tid, dqlog);
 #pragma unroll
-  for (int k = 0; k < M + L - 1; ++k) wv[k] = W4[(q0 + k * dq) & (NG - 1)];  // taps may wrap >1x
+  for (int k = K0; k < K1; ++k) wv[k] = W4[(q0 + k * dq) & (NG - 1)];  // taps may wrap >1x
+}
+
+template <int L, int M, int NG, bool PAD>
+__device__ __forceinline__ int chain_compute(const float4* __restrict__ V4, const float4 (&wv)[M + L - 1],
+                                             int dqlog, const float (&hs)[L], const FilterBank& fb,
+                                             int tid, float4 (&vreg)[M]) {
+  const int dq = 1 << dqlog;
+  const int q0 = chain_q0<M>(tid, dqlog);
+  float4 vv[M + L - 1];
 #pragma unroll
   for (int k = 0; k < M + L - 1; ++k) {
     const int qv = (q0 + k * dq) & (NG - 1);
@@ -461,18 +472,36 @@ __device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, co
   return q0;
 }
 
+template <int L, int M, int NG, bool PAD = false>
+__device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, const float4* __restrict__ W4,
+                                               int dqlog, const float (&hs)[L],
+                                               const FilterBank& fb, int tid, float4 (&vreg)[M]) {
+  static_assert((NG & (NG - 1)) == 0, "chain levels need a power-of-two group count");
+  float4 wv[M + L - 1];
+  chain_load_w<L, M, NG>(W4, dqlog, tid, wv);
+  return chain_compute<L, M, NG, PAD>(V4, wv, dqlog, hs, fb, tid, vreg);
+}
+
 // MODE 0: W_j copied global -> LDS at the start of each level.
 // MODE 1: as 0, but W_{j-1} is prefetched into registers while level j computes.
 // MODE 2: W_j taps read straight from global memory (L1/L2); LDS holds V only (n floats),
 //         so two workgroups fit per CU and one's loads overlap the other's math.
 // MODE 3: as 2, but levels with a whole-group dilation run along dilation chains
 //         (syn_level_chain: each W_j / V_j tap loaded ~2x instead of 8x).
+// MODE 6: as 3, and a chain level's W taps are loaded at the end of the level before
+//         (after its math, before its barrier and V write), so their latency overlaps the
+//         barrier wait, the V exchange and the V tap reads.
+// MODE 7: as 6 for the first 8 of the M+L-1 taps (register budget).
 template <int L, int GROUPS, int T, int MODE>
-__global__ void __launch_bounds__(T)
+__global__ void __launch_bounds__(T, MODE >= 6 ? 4 : 1)  // MODE 6/7: <= 128 VGPRs (2 workgroups per CU)
     imodwt_vec_kernel(const float* __restrict__ w, int n, int level, FilterBank fb, unsigned long long keep,
                       float* __restrict__ x, long long ld_out) {
   constexpr bool PREFETCH = MODE == 1;
   constexpr bool PAD = MODE >= 2;  // V alone in LDS: padded (vpad), see window_taps
+  constexpr bool CHAINS = MODE == 3 || MODE >= 6;
+  constexpr int PF = MODE == 7 ? 8 : GROUPS + L - 1;  // W taps loaded a level ahead
+  constexpr int NG = GROUPS * T;
+  constexpr int NGC = (NG & (NG - 1)) == 0 ? NG : 1;
   extern __shared__ __attribute__((aligned(16))) float4 sm4[];
   const int ng = n >> 2;
   float4* V4 = sm4;
@@ -487,6 +516,16 @@ __global__ void __launch_bounds__(T)
     const float4* vr = reinterpret_cast<const float4*>(win + static_cast<long long>(level) * n);
     for (int q = tid; q < ng; q += T) V4[vp(q)] = keepV ? vr[q] : z4;
   }
+  // chain level of dilation dm (log2 of dq in groups), or -1
+  auto chain_log = [&](int dm) {
+    if ((dm & 3) == 0 && NG == ng && (NG & (NG - 1)) == 0) {
+      const int dq = dm >> 2;
+      if (dq > 0 && (dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) return __builtin_ctz(dq);
+    }
+    return -1;
+  };
+  float4 wpre[GROUPS + L - 1];  // MODE 6: this level's W taps, loaded during the level before
+  bool have = false;
   float4 pre[GROUPS];
   if (PREFETCH) {
     const float4* wr = reinterpret_cast<const float4*>(win + static_cast<long long>(level - 1) * n);
@@ -511,17 +550,27 @@ __global__ void __launch_bounds__(T)
     int tl = tid;
     asm volatile("" : "+v"(tl));  // per-level copy: keeps address math out of LICM
     float4 vreg[GROUPS];
-    int dqlog = -1;
-    constexpr int NG = GROUPS * T;
-    if (MODE == 3 && (dm & 3) == 0 && NG == ng && (NG & (NG - 1)) == 0) {
-      const int dq = dm >> 2;
-      if ((dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) dqlog = __builtin_ctz(dq);
-    }
+    const int dqlog = CHAINS ? chain_log(dm) : -1;
     if (dqlog >= 0) {
       float hs[L];
 #pragma unroll
       for (int l = 0; l < L; ++l) hs[l] = wsel * fb.h[l];
-      const int q0 = syn_level_chain<L, GROUPS, (NG & (NG - 1)) == 0 ? NG : 1, PAD>(V4, wr, dqlog, hs, fb, tl, vreg);
+      int q0;
+      if constexpr (MODE >= 6) {
+        if (!have)
+          chain_load_w<L, GROUPS, NGC>(wr, dqlog, tl, wpre);
+        else if constexpr (PF < GROUPS + L - 1)
+          chain_load_w<L, GROUPS, NGC, PF>(wr, dqlog, tl, wpre);
+        q0 = chain_compute<L, GROUPS, NGC, PAD>(V4, wpre, dqlog, hs, fb, tl, vreg);
+        const int dn = j > 1 ? chain_log(dilation_mod(j - 1, n)) : -1;
+        have = dn >= 0;
+        asm volatile("" ::: "memory");  // after the level's math (pinned): wpre is free again
+        if (have)
+          chain_load_w<L, GROUPS, NGC, 0, PF>(reinterpret_cast<const float4*>(win + static_cast<long long>(j - 2) * n),
+                                              dn, tl, wpre);
+      } else {
+        q0 = syn_level_chain<L, GROUPS, NGC, PAD>(V4, wr, dqlog, hs, fb, tl, vreg);
+      }
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < GROUPS; ++k) V4[vp(q0 + (k << dqlog))] = vreg[k];
@@ -661,8 +710,12 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
       launch(imodwt_vec_kernel<8, 4, 1024, 0>, 1024);
     else if (var == 4)  // C3 A/B (ms): W from global, 2 WG/CU 2.00; W via LDS 2.11; + register prefetch 2.71
       launch_lds(imodwt_vec_kernel<8, 8, 512, 2>, 512, lds_pad);
-    else
+    else if (var == 6)  // all 15 taps a level ahead: 28 VGPRs spilled at the 128 cap, 2.22 ms
+      launch_lds(imodwt_vec_kernel<8, 8, 512, 6>, 512, lds_pad);
+    else if (var == 7)
       launch_lds(imodwt_vec_kernel<8, 8, 512, 3>, 512, lds_pad);
+    else  // one-process A/B (ms): MODE 3 1.506-1.508, MODE 7 1.492-1.495 (3 alternations)
+      launch_lds(imodwt_vec_kernel<8, 8, 512, 7>, 512, lds_pad);
   } else if (n_taps == 8) {
     allow_lds(imodwt_kernel<8>, lds);
     hipLaunchKernelGGL(imodwt_kernel<8>, dim3(batch), dim3(block), lds, st, w, ni, level, n_taps, fb,
