@@ -212,7 +212,7 @@ class C3:
         self.x = torch.tensor(synth_batch(rng, self.B, self.n), device=dev)
         self.units = self.B * (self.J + 1) * self.n
         self.bytes = self.B * self.n * 96  # 4 x + 44 W write + 44 W read + 4 x^
-        self.kernel = "modwt_vec_kernel<8,8,512,16>+imodwt_vec_kernel<8,8,512,7>"
+        self.kernel = "modwt_vec_kernel<8,8,512,16>+imodwt_vec_kernel<8,8,512,3>"
         self.per_step = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_vec_kernel<": 1}
         self.unit_name = "coeffs/s"
         self.bytes_note = "96 B per series-sample (x, W write, W read, x^)"

@@ -712,10 +712,11 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
       launch_lds(imodwt_vec_kernel<8, 8, 512, 2>, 512, lds_pad);
     else if (var == 6)  // all 15 taps a level ahead: 28 VGPRs spilled at the 128 cap, 2.22 ms
       launch_lds(imodwt_vec_kernel<8, 8, 512, 6>, 512, lds_pad);
-    else if (var == 7)
-      launch_lds(imodwt_vec_kernel<8, 8, 512, 3>, 512, lds_pad);
-    else  // one-process A/B (ms): MODE 3 1.506-1.508, MODE 7 1.492-1.495 (3 alternations)
+    else if (var == 7)  // one-process A/B (ms): MODE 3 1.506-1.508, MODE 7 1.492-1.495, but
+                        // FETCH_SIZE 6.32 -> 7.15 GB (the early taps fall out of L2 before use)
       launch_lds(imodwt_vec_kernel<8, 8, 512, 7>, 512, lds_pad);
+    else
+      launch_lds(imodwt_vec_kernel<8, 8, 512, 3>, 512, lds_pad);
   } else if (n_taps == 8) {
     allow_lds(imodwt_kernel<8>, lds);
     hipLaunchKernelGGL(imodwt_kernel<8>, dim3(batch), dim3(block), lds, st, w, ni, level, n_taps, fb,
