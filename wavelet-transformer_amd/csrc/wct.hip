@@ -226,7 +226,7 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
   const int n0 = a.n0;
   if (a.out_pow) put_row<LOGN, BUF>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w[m]); });
   if (a.out_sig)  // phase angle
-    put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return atan2f(w[m].y, w[m].x); });
+    put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return fast_atan2f(w[m].y, w[m].x); });
   if (a.out_u) {
     put_row<LOGN, BUF>(a.out_u + rowbase, t, n0, [&](int m) {
       const float r = sqrtf(cabs2(w[m]));
