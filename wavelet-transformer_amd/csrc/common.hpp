@@ -22,6 +22,11 @@ __device__ __forceinline__ cpx cconj(cpx a) { return a * cpx{1.f, -1.f}; }
 __device__ __forceinline__ cpx cscale(cpx a, float s) { return a * s; }
 __device__ __forceinline__ float cabs2(cpx a) { return fmaf(a.x, a.x, a.y * a.y); }
 
+// x / d by the hardware reciprocal (1 ulp) and one multiply: ~2 ulp instead of the
+// ~10-instruction IEEE division sequence.  Same 0/0 = NaN and x/0 = inf; differs only for
+// d below FLT_MIN (signal powers at ~1e-19 in fp32, meaningless at this precision anyway).
+__device__ __forceinline__ float fast_div(float x, float d) { return x * __builtin_amdgcn_rcpf(d); }
+
 // atan2(y, x) for finite inputs, |error| <= 5e-7 rad (the phase outputs' tolerance is
 // 1e-4): octant reduction to a = min/max in [0, 1] (hardware reciprocal, 1 ulp) and
 // atan(a) = a P(a^2), P a degree-7 fit of relative error 2e-7 in fp32 evaluation.

@@ -619,7 +619,7 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
         for (int c = 0; c < C; ++c) {
           const float s1 = acc[0][2 * c], s2 = acc[0][2 * c + 1];
           const float re = acc[1][2 * c], im = acc[1][2 * c + 1];
-          o[c] = (re * re + im * im) / (s1 * s2);
+          o[c] = fast_div(re * re + im * im, s1 * s2);
         }
         float* orow = out + static_cast<long long>(i) * n0;
         if constexpr (C == 2)
@@ -692,7 +692,7 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
     smooth_from_band<LOGN, Q, TWL, false>(v, yw, slot, my, tw, t, par, twl);
     if (valid) {
       const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
-      put_row<LOGN, BUF>(coh + rowbase, t, a.n0, [&](int m) { return cabs2(v[m]) / den[m]; });
+      put_row<LOGN, BUF>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
     }
   }
 }
