@@ -765,11 +765,15 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int*
   }
   const int rows = G::ROWS;
   const char* ev = getenv("WTMI_WCT_TARGET_WG");
-  // phase A rows are 6 FFTs each: more, shorter workgroups balance better here
-  // (C4 ms: 1024 WG 6.27, 2048 6.19, 4096 6.16, 8192 6.02)
-  const long long target = ev ? atoll(ev) : 8192;
+  // Row costs differ a lot (full-band rows several transforms, band rows few): more,
+  // shorter workgroups balance better.  C4 ms (one box, two alternations): target 2048
+  // 5.10, 4096 4.53-4.58, 8192 4.11-4.23, 12800 (= 4 rows each) 4.08-4.11; 4 rows each
+  // 3.95-4.09 vs 3 rows 4.01-4.09, 2 rows 4.03-4.13.  Default: 4-row workgroups.
+  const long long target = ev ? atoll(ev) : (1ll << 30);
   long long want = (target + a.batch - 1) / a.batch;
-  const int max_chunks = (a.S + 4 * rows - 1) / (4 * rows);
+  const char* mr = getenv("WTMI_WCT_MIN_ROWS");
+  const int min_rows = mr && atoi(mr) > 0 ? atoi(mr) : 4;  // rows per workgroup, at least
+  const int max_chunks = (a.S + min_rows * rows - 1) / (min_rows * rows);
   int nch = static_cast<int>(want < 1 ? 1 : want);
   if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
   int chunk = (a.S + nch - 1) / nch;
