@@ -20,6 +20,7 @@ import torch
 
 from wtmi import ops, transforms
 from wtmi.wavelets import Morlet, as_morlet
+from src.utils.wavelet_helpers import plot_cone_of_influence, plot_signficance_levels
 
 logger = logging.getLogger(__name__)
 
@@ -77,8 +78,9 @@ def run_cwt(cwt_data: Type[DataForCWT], normalize: bool = True, standardize: boo
     y = transforms._to_dev(np.asarray(cwt_data.y_values)).reshape(1, -1)
     mom_y = ops.series_moments(y)
     if standardize:
-        kw = {k: kwargs[k] for k in ("detrend", "standardize", "remove_mean") if k in kwargs}
-        coef = transforms.standardize_coefs(mom_y, **kw)
+        # kwargs go to standardize_series as in the reference (:102): an unknown keyword
+        # raises TypeError there and here
+        coef = transforms.standardize_coefs(mom_y, **kwargs)
         x32 = ops.affine(y, coef, torch.float32)
     else:  # quirk B.1: `normalize` has no effect
         x32 = ops.affine(y, torch.tensor([[0.0, 0.0, 1.0]], dtype=torch.float64, device=y.device),
@@ -99,3 +101,27 @@ def run_cwt(cwt_data: Type[DataForCWT], normalize: bool = True, standardize: boo
     sig = transforms._np(res["sig"][0], np.float64) if calculate_significance else None
     coi = transforms.cone_of_influence(n0, DT, mother)
     return ResultsFromCWT(power, 1 / freqs, sig, coi)
+
+
+def plot_cwt(cwt_ax, cwt_data: Type[DataForCWT], cwt_results: Type[ResultsFromCWT],
+             include_significance: bool = True, include_cone_of_influence: bool = True,
+             **kwargs) -> None:
+    """Filled contours of log2 power over (time, log2 period) at log2(levels), the
+    significance contour and the COI shading, period axis inverted with one tick per
+    octave (src/cwt.py:138-185).  kwargs: ``cmap`` plus the helpers' keys."""
+    log_period = np.log2(cwt_results.period)
+    cwt_ax.contourf(cwt_data.time_range, log_period, np.log2(cwt_results.power),
+                    np.log2(cwt_data.levels), extend="both", cmap=kwargs["cmap"])
+    if include_significance:
+        plot_signficance_levels(cwt_ax, cwt_results.significance_levels, cwt_data.time_range,
+                                cwt_results.period, **kwargs)
+    if include_cone_of_influence:
+        plot_cone_of_influence(cwt_ax, cwt_results.coi, cwt_data.time_range, cwt_data.levels,
+                               cwt_results.period, cwt_data.delta_t, tranform_type="cwt",
+                               **kwargs)
+    bottom, top = cwt_ax.get_ylim()
+    cwt_ax.set_ylim(top, bottom)  # short periods at the top
+    octave = 2 ** np.arange(np.ceil(np.log2(cwt_results.period.min())),
+                            np.ceil(np.log2(cwt_results.period.max())))
+    cwt_ax.set_yticks(np.log2(octave))
+    cwt_ax.set_yticklabels(octave, size=15)

@@ -18,6 +18,7 @@ import numpy.typing as npt
 
 from wtmi import transforms
 from wtmi.wavelets import Wavelet, as_filter_bank
+from src.utils.wavelet_helpers import align_series
 
 logger = logging.getLogger(__name__)
 
@@ -89,3 +90,47 @@ def run_dwt(dwt_data: Type[DataForDWT]) -> Type[ResultsFromDWT]:
 def reconstruct_signal_component(signal_coeffs: list, wavelet: str, level: int):
     """Inverse DWT keeping only list entry ``level`` (src/dwt.py:110-120)."""
     return transforms.waverec_variants(signal_coeffs, wavelet, [1 << level])[0]
+
+
+def _subplots(nrows, **kwargs):
+    import matplotlib.pyplot as plt  # plotting only; the transforms never import matplotlib
+    return plt.subplots(nrows, 1, **kwargs)
+
+
+def plot_components(label: str, coeffs: npt.NDArray, time: npt.NDArray, levels: int,
+                    wavelet: str, **kwargs):
+    """One panel per component: the smooth S_J on top, then D_J .. D_1, each trimmed
+    to the time axis (src/dwt.py:123-156).  All levels+1 single-entry reconstructions
+    come from ONE batched inverse-DWT launch."""
+    import matplotlib.pyplot as plt
+    fig, ax = _subplots(levels + 1, **kwargs)
+    parts = transforms.waverec_variants(coeffs, wavelet, [1 << lvl for lvl in range(levels + 1)])
+    logger.warning("lengths x: %s, t: %s", len(parts[0]), len(time))
+    for lvl in range(levels + 1):
+        y = parts[lvl]
+        if len(y) != len(time):
+            y = align_series(time, y)
+        ax[lvl].plot(time, y, label=label)
+        title = rf"$S_{{{levels}}}$" if lvl == 0 else rf"$D_{{{levels + 1 - lvl}}}$"
+        ax[lvl].set_title(title, size=15)
+    plt.legend(loc="upper left")
+    return fig
+
+
+def plot_smoothing(smooth_signals: dict, original_t: npt.NDArray, original_y: npt.NDArray,
+                   ascending: bool = False, **kwargs):
+    """One panel per smoothed signal over the original (src/dwt.py:159-184); panel
+    order follows the dict, reversed when ``ascending``."""
+    fig, axs = _subplots(len(smooth_signals), **kwargs)
+    items = list(smooth_signals.items())
+    if ascending:
+        items = items[::-1]
+    for panel, (level, signal) in enumerate(items):
+        axs[panel].plot(original_t, original_y, label="Original")
+        axs[panel].plot(original_t, signal["signal"])
+        axs[panel].set_title(rf"Approximation: $S_{{j-{len(smooth_signals) - level}}}$", size=15)
+        if panel == 0:
+            axs[panel].legend(loc="upper right")
+        else:
+            axs[panel].legend("", frameon=False)
+    return fig

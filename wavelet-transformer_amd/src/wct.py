@@ -20,7 +20,8 @@ import numpy.typing as npt
 import torch
 
 from wtmi import ops, transforms
-from wtmi.wavelets import Morlet, as_morlet
+from wtmi.wavelets import DOG, MexicanHat, Morlet, Paul, as_morlet
+from src.utils import wavelet_helpers
 
 logger = logging.getLogger(__name__)
 
@@ -28,7 +29,12 @@ DT = 1 / 12
 DJ = 1 / 8
 S0 = 2 * DT
 MOTHER = "morlet"
-MOTHER_DICT = {"morlet": Morlet(6)}
+MOTHER_DICT = {  # only "morlet" is transformable; the others raise in run_wct
+    "morlet": Morlet(6),
+    "paul": Paul(),
+    "DOG": DOG(),
+    "mexicanhat": MexicanHat(),
+}
 LEVELS = [0.0625, 0.125, 0.25, 0.5, 1, 2, 4, 8, 16]
 WCT_LEVELS = [0.0, 0.125, 0.25, 0.375, 0.5, 0.625, 0.75, 0.875, 1.0]
 
@@ -111,3 +117,36 @@ def run_wct(wavelet_coherence_transform: Type[DataForWCT], calculate_signficance
 def calculate_phase_difference(wct_phase: npt.NDArray) -> Tuple[npt.NDArray, npt.NDArray]:
     angle = 0.5 * np.pi - wct_phase
     return np.cos(angle), np.sin(angle)
+
+
+def plot_wct(wct_ax, wct_data: Type[DataForWCT], wct_results: Type[ResultsFromWCT],
+             include_significance: bool = True, include_cone_of_influence: bool = True,
+             include_phase_difference: bool = True, **kwargs) -> None:
+    """Filled contours of |coherence| at WCT_LEVELS over (time, log2 period), the
+    significance contour, the COI shading built like the CWT's ("cwt") and the phase
+    arrows (src/wct.py:161-224)."""
+    t, period = wct_data.t_values, wct_results.period
+    wct_ax.contourf(t, np.log2(period), np.abs(wct_results.coherence), WCT_LEVELS,
+                    extend="both", cmap=kwargs["cmap"],
+                    extent=[min(t), max(t), min(wct_results.coi), max(period)])
+    if include_significance:
+        wavelet_helpers.plot_signficance_levels(wct_ax, wct_results.significance_levels, t,
+                                                period, **kwargs)
+    if include_cone_of_influence:
+        wavelet_helpers.plot_cone_of_influence(wct_ax, wct_results.coi, t, wct_data.levels, period,
+                                               wct_data.delta_t, tranform_type="cwt", **kwargs)
+    if include_phase_difference:
+        plot_phase_difference(wct_ax, t, period, wct_results.phase_diff_u,
+                              wct_results.phase_diff_v, **kwargs)
+
+
+def plot_phase_difference(wct_ax, t_values: npt.NDArray, period: npt.NDArray,
+                          phase_diff_u: npt.NDArray, phase_diff_v: npt.NDArray, **kwargs) -> None:
+    """Phase arrows thinned to about 48 columns x 12 rows (src/wct.py:227-265)."""
+    rows, cols = phase_diff_u.shape
+    ys, xs = max(1, rows // 12), max(1, cols // 48)
+    wct_ax.quiver(t_values[::xs], np.log2(period[::ys]),
+                  phase_diff_u[::ys, ::xs], phase_diff_v[::ys, ::xs],
+                  units=kwargs["phase_diff_units"], angles=kwargs["phase_diff_angles"],
+                  pivot=kwargs["phase_diff_pivot"], linewidth=kwargs["phase_diff_linewidth"],
+                  edgecolor=kwargs["phase_diff_edgecolor"], alpha=kwargs["phase_diff_alpha"])

@@ -19,7 +19,8 @@ import numpy.typing as npt
 import torch
 
 from wtmi import ops, transforms
-from wtmi.wavelets import Morlet, as_morlet
+from wtmi.wavelets import DOG, MexicanHat, Morlet, Paul, as_morlet
+from src.utils import wavelet_helpers
 from src.utils.wavelet_helpers import coi_polygon
 
 logger = logging.getLogger(__name__)
@@ -28,7 +29,12 @@ DT = 1 / 12
 DJ = 1 / 8
 S0 = 2 * DT
 MOTHER = "morlet"
-MOTHER_DICT = {"morlet": Morlet(6)}
+MOTHER_DICT = {  # only "morlet" is transformable; the others raise in run_xwt
+    "morlet": Morlet(6),
+    "paul": Paul(),
+    "DOG": DOG(),
+    "mexicanhat": MexicanHat(),
+}
 LEVELS = [0.0625, 0.125, 0.25, 0.5, 1, 2, 4, 8, 16]
 
 XWT_PLOT_PROPS = {
@@ -119,3 +125,37 @@ def calculate_phase_difference(xwt_phase: npt.NDArray) -> Tuple[npt.NDArray, npt
     """Arrow components (Torrence & Webster 1999): u = cos(pi/2 - phase), v = sin(...)."""
     angle = 0.5 * np.pi - xwt_phase
     return np.cos(angle), np.sin(angle)
+
+
+def plot_xwt(xwt_ax, xwt_data: Type[DataForXWT], xwt_results: Type[ResultsFromXWT],
+             include_significance: bool = True, include_cone_of_influence: bool = True,
+             include_phase_difference: bool = True, **kwargs) -> None:
+    """Filled contours of log2 cross power at log2(levels) over (time, log2 period),
+    then the significance contour, the COI polygon (already in log2 space, "xwt") and
+    the phase arrows (src/xwt.py:157-223)."""
+    t, period = xwt_data.t_values, xwt_results.period
+    xwt_ax.contourf(t, np.log2(period), np.log2(xwt_results.power), np.log2(xwt_data.levels),
+                    extend="both", cmap=kwargs["cmap"],
+                    extent=[min(t), max(t), min(xwt_results.coi), max(period)])
+    if include_significance:
+        wavelet_helpers.plot_signficance_levels(xwt_ax, xwt_results.significance_levels, t,
+                                                period, **kwargs)
+    if include_cone_of_influence:
+        wavelet_helpers.plot_cone_of_influence(xwt_ax, xwt_results.coi, t, xwt_data.levels, period,
+                                               xwt_data.delta_t, tranform_type="xwt", **kwargs)
+    if include_phase_difference:
+        plot_phase_difference(xwt_ax, t, period, xwt_results.phase_diff_u,
+                              xwt_results.phase_diff_v, **kwargs)
+
+
+def plot_phase_difference(xwt_ax, t_values: npt.NDArray, period: npt.NDArray,
+                          phase_diff_u: npt.NDArray, phase_diff_v: npt.NDArray, **kwargs) -> None:
+    """Phase arrows on a fixed decimation: every 12th sample, every 8th period and
+    every 12th row of u/v (src/xwt.py:226-253).  The u/v rows are at dj = 1/12 and the
+    periods at dj = 1/8 (quirk B.5), so the two decimations select the same number of
+    rows.  kwargs: ``phase_diff_{units,angles,pivot,linewidth,edgecolor,alpha}``."""
+    xwt_ax.quiver(t_values[::12], np.log2(period[::8]),
+                  phase_diff_u[::12, ::12], phase_diff_v[::12, ::12],
+                  units=kwargs["phase_diff_units"], angles=kwargs["phase_diff_angles"],
+                  pivot=kwargs["phase_diff_pivot"], linewidth=kwargs["phase_diff_linewidth"],
+                  edgecolor=kwargs["phase_diff_edgecolor"], alpha=kwargs["phase_diff_alpha"])

@@ -45,6 +45,67 @@ class Morlet:
         return f"Morlet(f0={self.f0:g})"
 
 
+class _Unsupported:
+    """Descriptor of a pycwt mother wavelet the engine does not transform (only the Morlet
+    Fourier filter is built into the CWT kernels).  Carries pycwt 0.4.0b0's constants so
+    that the reference's ``MOTHER_DICT`` keys exist (src/xwt.py:29-34, src/wct.py:36-41);
+    passing one to a transform raises ValueError, as for any non-Morlet wavelet."""
+
+    name = "unsupported"
+
+    def __repr__(self):
+        return f"{type(self).__name__}(m={self.m})"
+
+
+class Paul(_Unsupported):
+    """pycwt ``Paul(m=4)``: flambda = 4 pi / (2m + 1), coi = sqrt(2)."""
+
+    name = "Paul"
+
+    def __init__(self, m: int = 4):
+        self.m, self.dofmin = m, 2
+        if m == 4:
+            self.cdelta, self.gamma, self.deltaj0 = 1.132, 1.17, 1.5
+        else:
+            self.cdelta = self.gamma = self.deltaj0 = -1
+
+    def flambda(self) -> float:
+        return (4 * np.pi) / (2 * self.m + 1)
+
+    def coi(self) -> float:
+        return np.sqrt(2)
+
+
+class DOG(_Unsupported):
+    """pycwt ``DOG(m=2)`` (derivative of Gaussian): flambda = 2 pi / sqrt(m + 1/2)."""
+
+    name = "DOG"
+
+    def __init__(self, m: int = 2):
+        self.m, self.dofmin = m, 1
+        if m == 2:
+            self.cdelta, self.gamma, self.deltaj0 = 3.541, 1.43, 1.4
+        elif m == 6:
+            self.cdelta, self.gamma, self.deltaj0 = 1.966, 1.37, 0.97
+        else:
+            self.cdelta = self.gamma = self.deltaj0 = -1
+
+    def flambda(self) -> float:
+        return (2 * np.pi / np.sqrt(self.m + 0.5))
+
+    def coi(self) -> float:
+        return 1 / np.sqrt(2)
+
+
+class MexicanHat(DOG):
+    """pycwt ``MexicanHat()`` = DOG(m=2)."""
+
+    name = "Mexican Hat"
+
+    def __init__(self):
+        super().__init__(2)
+
+
 def as_morlet(wavelet) -> Morlet:
     """Accept a wtmi/pycwt Morlet object, the string 'morlet', or None (Morlet(6))."""
     if wavelet is None:
