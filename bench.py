@@ -5,10 +5,22 @@
 
 Default workload = BASELINE config 2 (the metric's single-GPU config): batched Morlet
 CWT, 1024 synthetic series x 4096 samples x 128 scales, fp32 in, complex64 W out,
-inputs resident in HBM, one step = one transform of the whole per-GPU batch.  With
-N > 1 (launched by torch.distributed.run) every rank transforms its own 1024-series
-shard (weak scaling, no collective on the data path); RCCL is used only for the
-barrier and the max-over-ranks of the timed region.
+inputs resident in HBM, one step = one transform of the whole batch.
+
+Multi-GPU: the config's GLOBAL batch (C2 1024 series, C3 8192, C4 512
+pairs, C5 65536) is split into contiguous per-rank blocks (wtmi.sharding.shard_range),
+strong scaling, no collective on the data path; RCCL carries only the barrier and the
+max-over-ranks of the timed region.  ``--gpus N`` works two ways:
+  * under ``torch.distributed.run --nproc-per-node N`` (RANK/WORLD_SIZE in the env):
+    this process is one rank; ``--gpus`` must equal WORLD_SIZE;
+  * as a plain ``python bench.py --gpus N``: this process starts N fresh rank processes
+    (before it, or they, touch the GPU), waits for them and exits with their status.
+``--scaling weak`` gives every rank the whole config batch instead.
+
+Clock ramp: the first few dozen launches after an idle period run ~10 % slower (C2:
+0.89 ms/step after 5 warm-up steps, 0.79 after 30 or 300, same box, same process
+order).  After the W requested warm-up steps the bench keeps stepping, untimed, until
+``--prewarm-s`` seconds (default 0.5) of warm-up have passed; the JSON line records it.
 
 Rank 0 prints ONE JSON line: value = all ranks' coefficients / max-over-ranks time,
 plus "roofline" (dominant kernel, HIP-event timed on its own stream) and
@@ -92,10 +104,35 @@ CPU_SAMPLE = {"c2": "pycwt.cwt restatement (scipy.fftpack, fp64), series x 4096 
                     "series x 16384 samples",
               "c4": "pycwt.wct(sig=False) restatement (2 CWTs + 3 Morlet.smooth, fp64), "
                     "pairs x 8192 samples x 97 scales"}
-CPU_PER_WORKER = {"c2": 32, "c5": 10, "c3": 2, "c4": 2}  # ~1 s per worker, ~16 s of CPU in all
+CPU_PER_WORKER = {"c2": 96, "c5": 24, "c3": 3, "c4": 3}  # ~1-2 s of CPU per worker
 
 
-def cpu_baseline(cfg, per_worker, workers):
+def host_cpu_info():
+    """Cores this process may use (affinity, capped by a cgroup CPU quota if any) and the
+    CPU model, for the cpu_baseline record."""
+    visible = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = min(visible, quota) if quota else visible
+    return {"usable": usable, "affinity": visible, "cgroup_quota": quota, "model": model}
+
+
+def cpu_baseline(cfg, per_worker, workers, info):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     per_worker = per_worker or CPU_PER_WORKER[cfg]
@@ -107,6 +144,8 @@ def cpu_baseline(cfg, per_worker, workers):
     busy = max(r[0] for r in res)
     units = sum(r[1] for r in res)
     return {"value": units / busy, "unit": "coeffs/s", "cores": workers, "kind": "port",
+            "cpu_model": info["model"], "host_cpus_affinity": info["affinity"],
+            "cgroup_cpu_quota": info["cgroup_quota"],
             "sample": f"{workers * per_worker} x {CPU_SAMPLE[cfg]}; {workers} single-threaded "
                       f"processes x {per_worker}; rate = coefficients / slowest worker's compute "
                       f"time (pool wall {wall:.1f} s)",
@@ -114,170 +153,242 @@ def cpu_baseline(cfg, per_worker, workers):
 
 
 # ------------------------------------------------------------------- workloads
-class C2:
-    """Batched Morlet CWT: 1024 x 4096 x 128 scales, complex64 W."""
-    name = "c2"
-    B, n0, dj, J = 1024, 4096, 1 / 12, 127
+GEN_BLOCK = 64  # rows per seeded generator block: a shard's rows do not depend on N
 
-    def __init__(self, rank, dev):
+
+def synth_rows(seed, lo, hi, n, pairs=False):
+    """Rows [lo, hi) of a config's global synthetic batch (series, or (y1, y2) pairs),
+    identical whichever rank or world size asks for them."""
+    b0, b1 = lo // GEN_BLOCK, -(-hi // GEN_BLOCK)
+    y1, y2 = [], []
+    for blk in range(b0, b1):
+        rng = np.random.default_rng([seed, blk])
+        a = synth_batch(rng, GEN_BLOCK, n)
+        y1.append(a)
+        if pairs:
+            y2.append((0.6 * np.roll(a, 3, axis=1) + 0.8 * synth_batch(rng, GEN_BLOCK, n))
+                      .astype(np.float32))
+    cut = slice(lo - b0 * GEN_BLOCK, hi - b0 * GEN_BLOCK)
+    if pairs:
+        return np.concatenate(y1)[cut], np.concatenate(y2)[cut]
+    return np.concatenate(y1)[cut]
+
+
+class Workload:
+    """One config's per-rank share: rows [lo, hi) of the global batch B (strong
+    scaling) or the whole batch on every rank (weak)."""
+    B = 0
+    seed = 0
+
+    def __init__(self, rank, world, dev, scaling):
         import torch
-        from wtmi import ops
-        self.ops, self.torch = ops, torch
-        rng = np.random.default_rng(1002 + 7919 * rank)
-        self.x = torch.tensor(synth_batch(rng, self.B, self.n0), device=dev)
+        from wtmi import ops, sharding
+        self.ops, self.torch, self.dev = ops, torch, dev
+        self.global_batch = self.B * (world if scaling == "weak" else 1)
+        if scaling == "weak":
+            self.lo, self.hi = 0, self.B
+        else:
+            self.lo, self.hi = sharding.shard_range(self.B, rank, world)
+        self.local = self.hi - self.lo
+        self.setup()
+
+    def shard_config(self, world, scaling):
+        return {"global_batch": self.global_batch, "per_rank_batch": self.local,
+                "rank0_rows": [self.lo, self.hi], "scaling": scaling,
+                "parallelism": f"{self.axis}-sharded x{world}, contiguous blocks, "
+                               "no collective on the data path"}
+
+
+class C2(Workload):
+    """Batched Morlet CWT: 1024 x 4096 x 128 scales, complex64 W."""
+    name, axis, seed = "c2", "series", 1002
+    B, n0, dj, J = 1024, 4096, 1 / 12, 127
+    kernel = "cwt_morlet_kernel<12,1,0,0>"
+
+    def setup(self):
+        torch = self.torch
+        self.x = torch.tensor(synth_rows(self.seed, self.lo, self.hi, self.n0), device=self.dev)
         self.sj = 2 * DT * 2 ** (np.arange(self.J + 1) * self.dj)
-        self.sjd = torch.tensor(self.sj, device=dev)
-        self.out = torch.empty((self.B, self.sj.size, self.n0), dtype=torch.complex64, device=dev)
-        self.units = self.B * self.sj.size * self.n0
-        self.bytes = self.units * 8 + self.B * self.n0 * 4  # W write + x read
-        self.kernel = "cwt_morlet_kernel<12,1,0,0>"
-        self.per_step = {"wtmi::cwt_morlet_kernel<12": 1}
-        self.unit_name = "coeffs/s"
+        self.sjd = torch.tensor(self.sj, device=self.dev)
+        self.out = torch.empty((self.local, self.sj.size, self.n0), dtype=torch.complex64,
+                               device=self.dev)
+        self.units = self.local * self.sj.size * self.n0
+        self.bytes = self.units * 8 + self.local * self.n0 * 4  # W write + x read
+        self.per_step = {"wtmi::" + self.kernel.split(",")[0]: 1}
         self.bytes_note = "8 B/coeff complex64 W write + 4 B/sample x read"
 
     def step(self):
-        self.ops.cwt_morlet(self.x, self.sjd, DT, 6.0, out_w=self.out)
+        if self.local:
+            self.ops.cwt_morlet(self.x, self.sjd, DT, 6.0, out_w=self.out)
+
+    def _oracle_rows(self, W, x):
+        from oracle import pycwt_spec as pc
+        ref = pc.cwt(x.astype(np.float64), DT, self.dj, 2 * DT, self.J)[0]
+        return float((np.linalg.norm(W.astype(np.complex128) - ref, axis=1)
+                      / np.linalg.norm(ref, axis=1)).max())
 
     def check(self):
-        """Cheap size-independent check on the timed output: row 0 vs oracle."""
-        from oracle import pycwt_spec as pc
-        W = self.out[0].cpu().numpy().astype(np.complex128)
-        ref = pc.cwt(self.x[0].cpu().numpy().astype(np.float64), DT, self.dj, 2 * DT, self.J)[0]
-        num = np.linalg.norm(W - ref, axis=1)
-        den = np.linalg.norm(ref, axis=1)
-        return float((num / den).max())
+        """First and last series of this rank's output vs the oracle (max row error)."""
+        rows = sorted({0, self.local - 1})
+        return max(self._oracle_rows(self.out[r].cpu().numpy(), self.x[r].cpu().numpy())
+                   for r in rows)
 
-    def config(self, world):
-        return {"workload": "C2: batched Morlet CWT (BASELINE configs[1])", "series_per_gpu": self.B,
-                "global_batch": self.B * world, "samples": self.n0, "scales": int(self.sj.size),
-                "dt": DT, "dj": self.dj, "s0": 2 * DT, "f0": 6.0, "output": "complex64 W",
-                "parallelism": f"series-sharded x{world} (no collective on the data path)"}
+    def config(self):
+        return {"workload": "C2: batched Morlet CWT (BASELINE configs[1])", "samples": self.n0,
+                "scales": int(self.sj.size), "dt": DT, "dj": self.dj, "s0": 2 * DT, "f0": 6.0,
+                "output": "complex64 W"}
 
 
 class C5(C2):
-    """Large-batch CWT: 8192 series/GPU x 8192 x 256 scales (dj = 1/24), streamed in
-    chunks of 512 series into a reused output buffer (one-box sweep, ms per step: chunk 256
-    27.9-28.0, 512 27.2-27.3, 1024 27.5)."""
-    name = "c5"
-    B, n0, dj, J = 8192, 8192, 1 / 24, 255
-    chunk = int(os.environ.get("WTMI_C5_CHUNK", "512"))
+    """Large-batch CWT: 65536 series x 8192 x 256 scales (dj = 1/24), each rank streaming
+    its series in chunks of 512 into one reused output buffer (one-box sweep, ms per 8192
+    series: chunk 256 27.9-28.0, 512 27.2-27.3, 1024 27.5)."""
+    name, axis, seed = "c5", "series", 1005
+    B, n0, dj, J = 65536, 8192, 1 / 24, 255
+    chunk = 512
+    kernel = "cwt_morlet_kernel<13,1,0,0>"
 
-    def __init__(self, rank, dev):
-        import torch
-        from wtmi import ops
-        self.ops, self.torch = ops, torch
-        rng = np.random.default_rng(1005 + 7919 * rank)
-        self.x = torch.tensor(synth_batch(rng, self.B, self.n0), device=dev)
+    def setup(self):
+        torch = self.torch
+        x = np.empty((self.local, self.n0), np.float32)
+        for c in range(0, self.local, 4096):  # bounded host temporaries
+            x[c:c + 4096] = synth_rows(self.seed, self.lo + c, min(self.hi, self.lo + c + 4096),
+                                       self.n0)
+        self.x = torch.tensor(x, device=self.dev)
+        del x
         self.sj = 2 * DT * 2 ** (np.arange(self.J + 1) * self.dj)
-        self.sjd = torch.tensor(self.sj, device=dev)
-        self.out = torch.empty((self.chunk, self.sj.size, self.n0), dtype=torch.complex64,
-                               device=dev)
-        self.units = self.B * self.sj.size * self.n0
-        self.bytes = self.units * 8 + self.B * self.n0 * 4
-        self.kernel = "cwt_morlet_kernel<13,1,0,0>"
-        self.per_step = {"wtmi::cwt_morlet_kernel<13": self.B // self.chunk}
-        self.unit_name = "coeffs/s"
+        self.sjd = torch.tensor(self.sj, device=self.dev)
+        self.out = torch.empty((min(self.chunk, max(self.local, 1)), self.sj.size, self.n0),
+                               dtype=torch.complex64, device=self.dev)
+        self.units = self.local * self.sj.size * self.n0
+        self.bytes = self.units * 8 + self.local * self.n0 * 4
+        self.per_step = {"wtmi::cwt_morlet_kernel<13": -(-self.local // self.chunk)}
         self.bytes_note = "8 B/coeff complex64 W write + 4 B/sample x read"
 
     def step(self):
-        for c in range(0, self.B, self.chunk):
-            self.ops.cwt_morlet(self.x[c:c + self.chunk], self.sjd, DT, 6.0, out_w=self.out)
+        for c in range(0, self.local, self.chunk):
+            e = min(self.local, c + self.chunk)
+            self.ops.cwt_morlet(self.x[c:e], self.sjd, DT, 6.0, out_w=self.out[:e - c])
 
     def check(self):
-        from oracle import pycwt_spec as pc
-        W = self.out[0].cpu().numpy().astype(np.complex128)  # last chunk, first series
-        x0 = self.x[self.B - self.chunk].cpu().numpy().astype(np.float64)
-        ref = pc.cwt(x0, DT, self.dj, 2 * DT, self.J)[0]
-        return float((np.linalg.norm(W - ref, axis=1) / np.linalg.norm(ref, axis=1)).max())
+        """The last chunk's first and last series (the buffer holds the last chunk)."""
+        c0 = (self.local - 1) // self.chunk * self.chunk
+        rows = sorted({0, self.local - 1 - c0})
+        return max(self._oracle_rows(self.out[r].cpu().numpy(), self.x[c0 + r].cpu().numpy())
+                   for r in rows)
 
-    def config(self, world):
-        d = super().config(world)
+    def config(self):
+        d = super().config()
         d.update(workload="C5: large-batch streamed Morlet CWT (BASELINE configs[4])",
                  chunk_series=self.chunk)
         return d
 
 
-class C3:
+class C3(Workload):
     """MODWT db4 J=10: 8192 x 16384, decompose + reconstruct."""
-    name = "c3"
+    name, axis, seed = "c3", "series", 1003
     B, n, J = 8192, 16384, 10
+    kernel = "modwt_vec_kernel<8,8,512,16>+imodwt_vec_kernel<8,8,512,3>"
 
-    def __init__(self, rank, dev):
-        import torch
-        from wtmi import ops
+    def setup(self):
         from wtmi.wavelets import Wavelet
-        self.ops, self.torch = ops, torch
         self.w = Wavelet("db4")
-        rng = np.random.default_rng(1003 + 7919 * rank)
-        self.x = torch.tensor(synth_batch(rng, self.B, self.n), device=dev)
-        self.units = self.B * (self.J + 1) * self.n
-        self.bytes = self.B * self.n * 96  # 4 x + 44 W write + 44 W read + 4 x^
-        self.kernel = "modwt_vec_kernel<8,8,512,16>+imodwt_vec_kernel<8,8,512,3>"
+        x = np.empty((self.local, self.n), np.float32)
+        for c in range(0, self.local, 1024):
+            x[c:c + 1024] = synth_rows(self.seed, self.lo + c, min(self.hi, self.lo + c + 1024), self.n)
+        self.x = self.torch.tensor(x, device=self.dev)
+        self.units = self.local * (self.J + 1) * self.n
+        self.bytes = self.local * self.n * 96  # 4 x + 44 W write + 44 W read + 4 x^
         self.per_step = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_vec_kernel<": 1}
-        self.unit_name = "coeffs/s"
         self.bytes_note = "96 B per series-sample (x, W write, W read, x^)"
 
     def step(self):
-        w = self.ops.modwt(self.x, self.w.dec_lo, self.w.dec_hi, self.J)
-        self.xr = self.ops.imodwt(w, self.w.dec_lo, self.w.dec_hi)
+        if self.local:
+            w = self.ops.modwt(self.x, self.w.dec_lo, self.w.dec_hi, self.J)
+            self.xr = self.ops.imodwt(w, self.w.dec_lo, self.w.dec_hi)
 
     def check(self):
         return float((self.xr - self.x).abs().max().item() / self.x.abs().max().item())
 
-    def config(self, world):
+    def config(self):
         return {"workload": "C3: MODWT db4 J=10 decompose+reconstruct (BASELINE configs[2])",
-                "series_per_gpu": self.B, "global_batch": self.B * world, "samples": self.n,
-                "levels": self.J, "parallelism": f"series-sharded x{world}"}
+                "samples": self.n, "levels": self.J}
 
 
-class C4:
+class C4(Workload):
     """XWT + WCT: 512 pairs x 8192, dj = 1/8 -> 97 scales."""
-    name = "c4"
-    P, n, dj = 512, 8192, 1 / 8
+    name, axis, seed = "c4", "pair", 1004
+    B, n, dj = 512, 8192, 1 / 8
+    kernel = "wct_plan<13>+wct_spectra<13>+wct_phase_a<13>+wct_phase_c<13>+wct_phase_b<10>"
 
-    def __init__(self, rank, dev):
-        import torch
-        from wtmi import ops, transforms
-        self.ops, self.T, self.torch = ops, transforms, torch
-        rng = np.random.default_rng(1004 + 7919 * rank)
-        y1 = synth_batch(rng, self.P, self.n)
-        y2 = (0.6 * np.roll(y1, 3, axis=1) + 0.8 * synth_batch(rng, self.P, self.n)).astype(np.float32)
+    def setup(self):
+        from wtmi import transforms
+        torch, dev = self.torch, self.dev
+        self.T = transforms
+        y1, y2 = synth_rows(self.seed, self.lo, self.hi, self.n, pairs=True)
         self.y1 = torch.tensor(y1, device=dev)
         self.y2 = torch.tensor(y2, device=dev)
         self.sj, _ = transforms.scales_for(self.n, DT, self.dj, 2 * DT, -1, transforms.as_morlet(None))
         S = self.sj.size
-        self.units = self.P * S * self.n
-        self.bytes = self.units * 12 + self.P * self.n * 8
-        self.ws = torch.empty(ops.wct_workspace_bytes(self.P, self.n, S), dtype=torch.uint8,
-                              device=dev)
-        self.kernel = "wct_plan<13>+wct_spectra<13>+wct_phase_a<13>+wct_phase_c<13>+wct_phase_b<10>"
+        self.units = self.local * S * self.n
+        self.bytes = self.units * 12 + self.local * self.n * 8
+        self.ws = torch.empty(self.ops.wct_workspace_bytes(max(self.local, 1), self.n, S),
+                              dtype=torch.uint8, device=dev)
         self.per_step = {"wtmi::wct_plan_kernel<": 1, "wtmi::wct_spectra<": 1, "wtmi::wct_phase_a<": 1,
                          "wtmi::wct_phase_c<": 1, "wtmi::wct_phase_b<": 1}
-        self.unit_name = "coeffs/s"
         self.bytes_note = "12 B/coeff (|W12|^2 + WCT + phase, f32) + 8 B/pair-sample inputs"
 
     def step(self):
         # one fused pass: XWT power |W1 W2*|^2, phase angle and WCT coherence
-        self.r = self.T.wct_batch(self.y1, self.y2, DT, self.dj, 2 * DT, -1, workspace=self.ws,
-                                  want_uv=False, want_power=True, want_phase=True)[0]
+        if self.local:
+            self.r = self.T.wct_batch(self.y1, self.y2, DT, self.dj, 2 * DT, -1, workspace=self.ws,
+                                      want_uv=False, want_power=True, want_phase=True)[0]
 
     def check(self):
-        """Pair 0's coherence vs the oracle's pycwt.wct restatement (max abs difference)."""
+        """First and last pair's coherence vs the oracle's pycwt.wct (max abs difference)."""
         from oracle import pycwt_spec as pc
-        y1 = self.y1[0].cpu().numpy().astype(np.float64)
-        y2 = self.y2[0].cpu().numpy().astype(np.float64)
-        ref = pc.wct(y1, y2, DT, dj=self.dj, s0=2 * DT, J=-1, sig=False)[0]
-        return float(np.abs(self.r["coh"][0].cpu().numpy() - ref).max())
+        err = 0.0
+        for p in sorted({0, self.local - 1}):
+            y1 = self.y1[p].cpu().numpy().astype(np.float64)
+            y2 = self.y2[p].cpu().numpy().astype(np.float64)
+            ref = pc.wct(y1, y2, DT, dj=self.dj, s0=2 * DT, J=-1, sig=False)[0]
+            err = max(err, float(np.abs(self.r["coh"][p].cpu().numpy() - ref).max()))
+        return err
 
-    def config(self, world):
-        return {"workload": "C4: XWT + WCT coherence (BASELINE configs[3])", "pairs_per_gpu": self.P,
-                "global_batch": self.P * world, "samples": self.n, "scales": int(self.sj.size),
-                "parallelism": f"pair-sharded x{world}"}
+    def config(self):
+        return {"workload": "C4: XWT + WCT coherence (BASELINE configs[3])", "samples": self.n,
+                "scales": int(self.sj.size)}
 
 
-CONFIGS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5}
-CHECK_NAME = {"c2": "max_row_rel_err_vs_oracle", "c5": "max_row_rel_err_vs_oracle",
-              "c3": "round_trip_max_err_rel_to_max_x", "c4": "pair0_coherence_max_abs_err_vs_oracle"}
+class Stub(Workload):
+    """CPU-only stand-in (tests of the launcher and sharding; never a bench line)."""
+    name, axis, seed = "stub", "series", 7
+    B, n = 10, 256
+    kernel = "stub"
+
+    def setup(self):
+        self.x = self.torch.tensor(synth_rows(self.seed, self.lo, self.hi, self.n), device=self.dev)
+        self.units = self.local * self.n
+        self.bytes = self.local * self.n * 8
+        self.per_step = {}
+        self.bytes_note = "stub"
+
+    def step(self):
+        self.y = self.torch.fft.rfft(self.x, dim=-1)
+
+    def check(self):
+        return float(self.x.sum().item())
+
+    def config(self):
+        return {"workload": "stub (CPU launcher test)", "samples": self.n}
+
+
+CONFIGS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5, "stub": Stub}
+CHECK_NAME = {"c2": "rank0_first_last_series_max_row_rel_err_vs_oracle",
+              "c5": "rank0_last_chunk_first_last_series_max_row_rel_err_vs_oracle",
+              "c3": "rank0_round_trip_max_err_rel_to_max_x",
+              "c4": "rank0_first_last_pair_coherence_max_abs_err_vs_oracle",
+              "stub": "rank0_sum"}
 
 
 def pmc_traffic(cfg, per_step):
@@ -285,6 +396,8 @@ def pmc_traffic(cfg, per_step):
     (profiles/rNN/pmc_traffic.json, written by scripts/pmc_traffic.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench), or None."""
     import glob
+    if not per_step:
+        return None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
         with open(path) as fh:
             ent = json.load(fh).get(cfg)
@@ -302,90 +415,162 @@ def pmc_traffic(cfg, per_step):
     return None, None
 
 
+# -------------------------------------------------------------------- launcher
+def launch_ranks(n, argv):
+    """``python bench.py --gpus N`` without torch.distributed.run: start N fresh rank
+    processes (this parent never initialises the GPU), stream their output, stop the
+    others as soon as one fails, and return the worst exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--prewarm-s", type=float, default=0.5,
+                    help="keep warming up (untimed) until this many seconds have passed")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--cpu-per-worker", type=int, default=0, help="0 = per-config default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo + the stub workload only (launcher tests)")
     args = ap.parse_args()
+    if args.device == "cpu" and args.config != "stub":
+        ap.error("--device cpu runs only --config stub")
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     wl_cls = CONFIGS[args.config]
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "stub":
         # before any GPU initialisation (spawned workers never touch the GPU)
-        workers = max(1, min(args.cpu_workers, len(os.sched_getaffinity(0))))
-        cpu = cpu_baseline(args.config, args.cpu_per_worker, workers)
+        info = host_cpu_info()
+        workers = args.cpu_workers or info["usable"]
+        cpu = cpu_baseline(args.config, args.cpu_per_worker, workers, info)
 
     import torch
     import torch.distributed as dist
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    if args.device == "cuda":
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        sync = torch.cuda.synchronize
+    else:
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.device == "cuda":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
-    wl = wl_cls(rank, dev)
-    torch.cuda.synchronize()
+    wl = wl_cls(rank, world, dev, args.scaling)
+    sync()
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if args.device == "cuda":
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
 
+    t_warm = time.perf_counter()
     for _ in range(args.warmup):
         wl.step()
-    torch.cuda.synchronize()
+    sync()
+    extra = 0
+    while time.perf_counter() - t_warm < args.prewarm_s:
+        wl.step()
+        sync()
+        extra += 1
     barrier()
-    torch.cuda.synchronize()
+    sync()
 
-    stream = torch.cuda.current_stream(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    if args.device == "cuda":
+        stream = torch.cuda.current_stream(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record(stream)
+        if args.device == "cuda":
+            evs[i][0].record(stream)
         wl.step()
-        evs[i][1].record(stream)
-    torch.cuda.synchronize()
+        if args.device == "cuda":
+            evs[i][1].record(stream)
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if args.device == "cuda":
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    else:
+        kern_ms = elapsed / max(args.steps, 1) * 1e3
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, float(wl.units)], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
-    check = wl.check() if rank == 0 else None
+        tt = t[:1].clone()
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        uu = t[1:].clone()
+        dist.all_reduce(uu, op=dist.ReduceOp.SUM)
+        tmax, units_all = float(tt.item()), float(uu.item())
+    else:
+        tmax, units_all = elapsed, float(wl.units)
+    check = wl.check() if rank == 0 and wl.local else None
 
     if rank == 0:
-        total_units = wl.units * args.steps * world
         achieved = wl.bytes / (kern_ms * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(args.config, wl.per_step)
+        cfg = wl.config()
+        cfg.update(wl.shard_config(world, args.scaling))
         line = {
             "metric": METRIC,
-            "value": total_units / tmax,
-            "unit": wl.unit_name,
+            "value": units_all * args.steps / tmax,
+            "unit": "coeffs/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm": {"min_seconds": args.prewarm_s, "extra_untimed_steps": extra},
             "ms_per_step": tmax / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: seeded AR(1) red noise (a=0.7) + 3 random sinusoids per series, "
                     "resident in HBM before timing",
-            "config": wl.config(world),
+            "config": cfg,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": tsrc,
+                         "traffic_source": tsrc, "scope": "rank 0's launches",
                          "kernel": wl.kernel, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": wl.bytes, "bytes_model": wl.bytes_note},
             "cpu_baseline": cpu,
@@ -394,7 +579,8 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

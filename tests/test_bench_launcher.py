@@ -1,0 +1,64 @@
+"""bench.py's multi-rank launcher and strong-scaling shards, on CPU (gloo, stub workload).
+
+`python bench.py --gpus N` must start N ranks itself when no torch.distributed.run
+environment is present, shard the config's GLOBAL batch contiguously, and report
+n_gpus = N with value = all ranks' units / max-over-ranks time.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "stub",
+                        "--device", "cpu", "--steps", "3", "--warmup", "1", "--prewarm-s", "0",
+                        *args], cwd=ROOT, env=e, capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+@pytest.mark.parametrize("n,per_rank", [(1, 10), (2, 5), (3, 4)])
+def test_gpus_flag_launches_that_many_ranks(n, per_rank):
+    r, d = _run("--gpus", str(n))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert d["n_gpus"] == n and d["scaling"] == "strong"
+    c = d["config"]
+    assert c["global_batch"] == 10 and c["per_rank_batch"] == per_rank
+    assert c["rank0_rows"] == [0, per_rank]
+    # value counts every rank's units: 10 series x 256 samples per step, all ranks together
+    assert d["value"] == pytest.approx(10 * 256 * 3 / (d["ms_per_step"] * 3 / 1e3), rel=1e-6)
+
+
+def test_weak_scaling_gives_every_rank_the_whole_batch():
+    r, d = _run("--gpus", "2", "--scaling", "weak")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert d["config"]["global_batch"] == 20 and d["config"]["per_rank_batch"] == 10
+
+
+def test_gpus_must_match_torchrun_world_size():
+    r, d = _run("--gpus", "1", env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2 and d is None and "WORLD_SIZE=2" in r.stderr
+
+
+def test_shard_rows_do_not_depend_on_world_size():
+    sys.path.insert(0, ROOT)
+    import numpy as np
+
+    import bench
+    whole = bench.synth_rows(5, 0, 200, 64)
+    parts = np.concatenate([bench.synth_rows(5, lo, hi, 64) for lo, hi in ((0, 67), (67, 134), (134, 200))])
+    np.testing.assert_array_equal(whole, parts)
+    a1, a2 = bench.synth_rows(9, 10, 90, 32, pairs=True)
+    b1, b2 = bench.synth_rows(9, 0, 100, 32, pairs=True)
+    np.testing.assert_array_equal(a1, b1[10:90])
+    np.testing.assert_array_equal(a2, b2[10:90])
