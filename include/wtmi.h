@@ -122,6 +122,17 @@ int wtmi_series_moments(const void* x, int x_is_f64, long long ld, long long bat
 int wtmi_affine(const void* x, int x_is_f64, long long ld_in, long long batch, long long n,
                 const double* coef, void* y, int y_is_f64, long long ld_out, void* stream);
 
+/* ---- launch options (no reference counterpart) ----------------------------------
+ * Launch-policy knobs, read from WTMI_<NAME> environment variables once at first use
+ * and settable here: cwt_prune (2 band rows + narrowed entry passes, 1 band rows, 0 full
+ * transforms), cwt_target_wg, wct_prune (1 / 0), wct_target_wg, wct_min_rows.  The prune
+ * switches exist so that tests can compare pruned and full transforms; results agree
+ * to fp32 resolution either way.  Not thread-safe against concurrent launches.
+ * wtmi_set_option: 0, or -1 for an unknown name / out-of-range value;
+ * wtmi_get_option: the value, or -1 for an unknown name.                             */
+int wtmi_set_option(const char* name, long long value);
+long long wtmi_get_option(const char* name);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,8 +30,6 @@ for s in $STEPS; do
         done
         python scripts/pmc_traffic.py $c $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/pmc_traffic.json || exit 1
       done ;;
-    sweep) step sweep 600 python scripts/cwt_sweep.py || exit $? ;;
-    diag)  step diag 600 python scripts/cwt_diag.py --mode seq || exit $? ;;
     counters) step counters 300 rocprofv3 -L ;;
     pmc)
       i=0
@@ -39,15 +37,10 @@ for s in $STEPS; do
       IFS=';' read -ra GRPS <<< "$GROUPS_STR"
       for grp in "${GRPS[@]}"; do
         i=$((i+1))
-        step pmc$i 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/pmc$i -o run -- ${PMC_CMD:-python scripts/cwt_diag.py --mode short}
+        step pmc$i 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/pmc$i -o run -- ${PMC_CMD:-python bench.py --steps 3 --warmup 1 --no-cpu-baseline}
         rc=$?; [ $rc -ge 124 ] && exit $rc
       done ;;
     c3|c4|c5) step bench_$s 600 python bench.py --config $s --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
-    c3v)
-      for v in 0 1; do
-        WTMI_MODWT_VARIANT=$v WTMI_IMODWT_VARIANT=$v step bench_c3_var$v 300 python bench.py --config c3 --steps 20 --warmup 5 --no-cpu-baseline || exit $?
-      done ;;
-    mdiag) step modwt_diag 300 python scripts/modwt_diag.py --variants ${VARIANTS:-0,1,2,3} || exit $? ;;
     profcfg) step prof_$PCFG 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$PCFG -o run -- python bench.py --config $PCFG --steps 10 --warmup 3 --no-cpu-baseline || exit $? ;;
     profc3) step profc3 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc3 -o run -- python bench.py --config c3 --steps 10 --warmup 3 --no-cpu-baseline || exit $? ;;
     profall) step profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profall -o run -- python scripts/profile_all.py || exit $? ;;

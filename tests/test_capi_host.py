@@ -123,3 +123,20 @@ def test_torch_custom_ops_registered_and_gpu_only():
     if not torch.cuda.is_available():
         with pytest.raises(RuntimeError, match="GPU"):
             torch.ops.wtmi.cwt(torch.zeros(1, 32), torch.ones(3, dtype=torch.float64), 1.0, 6.0)
+
+
+def test_launch_options_set_get_and_reject():
+    """Options are read once from the environment and changed only through the ABI."""
+    from wtmi import _lib
+    assert _lib.get_option("cwt_prune") in (0, 1, 2)
+    with _lib.option("cwt_prune", 0):
+        assert _lib.get_option("cwt_prune") == 0
+        with _lib.option("wct_min_rows", 7):
+            assert _lib.get_option("wct_min_rows") == 7
+    assert _lib.get_option("wct_min_rows") == 4
+    lib = _lib.load()
+    assert lib.wtmi_set_option(b"cwt_prune", 3) == -1  # out of range
+    assert lib.wtmi_set_option(b"no_such_option", 1) == -1
+    assert lib.wtmi_get_option(b"no_such_option") == -1
+    with pytest.raises(_lib.WtmiError):
+        _lib.get_option("no_such_option")

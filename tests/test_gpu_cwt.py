@@ -55,7 +55,7 @@ def test_cwt_rows_match_oracle(n0, dj, J):
 
 @pytest.mark.parametrize("n0,dj,J,offset", [(4096, 1 / 12, 127, 0.0), (4096, 1 / 12, 127, 500.0),
                                             (8192, 1 / 24, 255, 0.0), (2000, 1 / 12, 110, 50.0)])
-def test_band_pruned_rows(n0, dj, J, offset, monkeypatch):
+def test_band_pruned_rows(n0, dj, J, offset):
     """Rows whose filtered spectrum lies in bins [0, N/16^q) enter the inverse FFT at pass q
     (cwt_common.hpp band_regime); full-band rows run a first pass over their NZ non-zero
     inputs only (first_pass_nz).  Random walks with a large mean put most of the energy at
@@ -68,11 +68,12 @@ def test_band_pruned_rows(n0, dj, J, offset, monkeypatch):
     dt, s0 = 1 / 12, 2 / 12
     sj = _scales(n0, dt, dj, s0, J)
     xd = torch.tensor(x, device="cuda")
-    monkeypatch.setenv("WTMI_CWT_PRUNE", "0")
-    full = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
-    for mode in ("1", "2"):  # band-pruned rows; + narrowed first passes of full-band rows
-        monkeypatch.setenv("WTMI_CWT_PRUNE", mode)
-        pr = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
+    from wtmi import _lib
+    with _lib.option("cwt_prune", 0):
+        full = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
+    for mode in (1, 2):  # band-pruned rows; + narrowed first passes of full-band rows
+        with _lib.option("cwt_prune", mode):
+            pr = _ops().cwt_morlet(xd, sj, dt)["w"].cpu().numpy()
         assert row_relerr(pr.astype(np.complex128), full.astype(np.complex128)).max() < TOL, mode
         for b in range(B):
             ref = pc.cwt(x[b].astype(np.float64), dt, dj, s0, J)[0]

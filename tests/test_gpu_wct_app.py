@@ -81,7 +81,7 @@ def test_wct_fused_power_and_phase_outputs(n, B):
 
 @pytest.mark.parametrize("n,dj", [(4096, 1 / 12), (8000, 1 / 8), (8192, 1 / 8), (3000, 1 / 16),
                                   (16384, 1 / 4)])
-def test_wct_band_paths_match_unpruned(n, dj, monkeypatch):
+def test_wct_band_paths_match_unpruned(n, dj):
     """Band-pruned transforms, the spectral-correlation rows of phase A and phase C's
     band-spectrum coherence against the unpruned path (six full transforms per row, every
     output row through phase B).  Boxcar widths 14, 10, 19 and 5 rows; padded and full rows."""
@@ -92,12 +92,13 @@ def test_wct_band_paths_match_unpruned(n, dj, monkeypatch):
     y1 = torch.tensor(np.stack([p[0] for p in pairs]), device="cuda", dtype=torch.float32)
     y2 = torch.tensor(np.stack([p[1] for p in pairs]), device="cuda", dtype=torch.float32)
     out = {}
-    for prune in ("0", "1"):
-        monkeypatch.setenv("WTMI_WCT_PRUNE", prune)
-        res, _, _ = transforms.wct_batch(y1, y2, 1 / 12, dj, 2 / 12, -1, want_uv=False,
-                                         want_power=True, want_phase=True)
+    from wtmi import _lib
+    for prune in (0, 1):
+        with _lib.option("wct_prune", prune):
+            res, _, _ = transforms.wct_batch(y1, y2, 1 / 12, dj, 2 / 12, -1, want_uv=False,
+                                             want_power=True, want_phase=True)
         out[prune] = {k: v.cpu().numpy().astype(np.float64) for k, v in res.items()}
-    full, band = out["0"], out["1"]
+    full, band = out[0], out[1]
     assert np.abs(full["coh"] - band["coh"]).max() <= 2e-5
     assert row_relerr(band["power"], full["power"]).max() < 2e-5
     mask = full["power"] > 1e-6 * full["power"].max(axis=-1, keepdims=True)

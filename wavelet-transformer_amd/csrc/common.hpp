@@ -98,6 +98,18 @@ enum : int {
   kErrUnsupported = -2 // size outside what the kernels handle
 };
 
+// Launch-policy knobs, read from the environment ONCE (first use) and settable through
+// wtmi_set_option (options.hip); never read per launch.  prune flags exist so tests can
+// compare the pruned transforms with full ones; the others are tuning defaults.
+struct Options {
+  int cwt_prune = 2;        // WTMI_CWT_PRUNE: 2 band rows + narrowed entry passes, 1 band rows, 0 full
+  int cwt_target_wg = 0;    // WTMI_CWT_TARGET_WG: workgroups per CWT launch, 0 = by size
+  int wct_prune = 1;        // WTMI_WCT_PRUNE: 1 band-pruned WCT rows, 0 full
+  int wct_target_wg = 0;    // WTMI_WCT_TARGET_WG: 0 = as many as wct_min_rows allows
+  int wct_min_rows = 4;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least
+};
+const Options& options();
+
 inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? kOk : static_cast<int>(e);

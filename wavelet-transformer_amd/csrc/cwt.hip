@@ -154,18 +154,6 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
   cpx* my = lds + g * P::PADN;
   constexpr int bufstride = G::ROWS * P::PADN;
 
-  if (a.diag & 4) {  // diagnostics: the kernel's row stores alone (no tables, no transforms)
-    const int kind = (a.out_w ? kOutW : 0) | (a.out_pow ? kOutPow : 0);
-    for (int jl = g; jl < j1 - j0; jl += G::ROWS) {
-      cpx v[16];
-#pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = mkc(static_cast<float>(jl), static_cast<float>(m));
-      const long long rowbase = (b * a.S + j0 + jl) * static_cast<long long>(a.n0);
-      if (a.n0 == P::N) store_any<LOGN, true>(v, a, kind, rowbase, 0.f, t);
-    }
-    return;
-  }
-
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const double s = a.scales[j0 + i];
     const cpx mp = morlet_params(s, a.dt, P::N);
@@ -200,10 +188,6 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
     add_mean_spectrum<LOGN>(X2, mu2, a.n0, t);
   }
   __syncthreads();  // prm_tab visible (the FFT barriers may be absent for N = 16)
-  if (a.diag & 8) {  // diagnostics: start-up only (tables, twiddles, load, forward FFT)
-    if (X[0].x == -1.2345e30f) a.out_w[0] = X[1];
-    return;
-  }
 
   const int kind = (a.out_w ? kOutW : 0) | (a.out_pow ? kOutPow : 0) | (a.out_sig ? kOutSig : 0) |
                    (a.out_u ? kOutUV : 0);
@@ -226,12 +210,7 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
       if (jj < j1 - j0) q = min(q, static_cast<int>(prm_tab[jj].w));
     }
     cpx v[16];
-    if (a.diag & 1) {
-#pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = X[m] * prm.x;
-    } else {
-      inverse_row<LOGN, NBUF, TWL>(v, X, prm, f0, q, my, bufstride, tw, t, par, twl);
-    }
+    inverse_row<LOGN, NBUF, TWL>(v, X, prm, f0, q, my, bufstride, tw, t, par, twl);
     if constexpr (MODE == 1) {
       cpx w1[16];
 #pragma unroll
@@ -241,7 +220,6 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
       for (int m = 0; m < 16; ++m) v[m] = cmul(w1[m], cconj(v[m]));
     }
     if (!valid) continue;
-    if ((a.diag & 2) && v[0].x != -1.2345e30f) continue;
     const int j = j0 + jl;
     const long long rowbase = (b * a.S + j) * static_cast<long long>(a.n0);
     const float sg = prm4.z;
@@ -315,11 +293,6 @@ static int log2_ceil(long long n) {
   return l;
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* s = getenv(name);
-  return s ? atoi(s) : dflt;
-}
-
 template <int LOGN, int NBUF, int MODE, int VAR = 0>
 static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   using G = CwtGeom<LOGN, MODE, VAR>;
@@ -329,7 +302,7 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   // Few, long workgroups: each one's start-up (twiddles, forward FFT) amortises over
   // more scales.  Measured (ms): C2 (LOGN 12, 3 WG/CU) 1024 WG 0.871, 2048 0.839,
   // 4096 0.860; C5 chunk (LOGN 13, 2 WG/CU) 512 30.9, 1024 30.86, 2048 31.2, 4096 32.9.
-  const int target = env_int("WTMI_CWT_TARGET_WG", LOGN >= 13 ? 1024 : 2048);
+  const int target = options().cwt_target_wg > 0 ? options().cwt_target_wg : (LOGN >= 13 ? 1024 : 2048);
   long long want = (target + a.batch - 1) / a.batch;
   const int max_chunks = (a.S + 4 * rows - 1) / (4 * rows);
   int nch = static_cast<int>(want < 1 ? 1 : want);
@@ -341,8 +314,7 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   a.nchunks = nch;
   a.chunk = chunk;
   // 2: band-pruned rows and narrowed first passes; 1: band-pruned rows only; 0: full FFTs
-  a.prune = env_int("WTMI_CWT_PRUNE", 2);
-  a.diag = env_int("WTMI_CWT_DIAG", 0);
+  a.prune = options().cwt_prune;
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
   hipLaunchKernelGGL((cwt_morlet_kernel<LOGN, NBUF, MODE, VAR>), dim3(static_cast<unsigned>(grid)),
@@ -362,11 +334,9 @@ static int dispatch(CwtArgs& a, hipStream_t st) {
                        0, st, a, N);
     return launch_status();
   }
-  const int nbuf = env_int("WTMI_CWT_NBUF", 1);
-#define WTMI_CASE(L)                                                   \
-  case L:                                                              \
-    return nbuf == 2 && L <= 13 ? launch_fft_cwt<L, (L <= 13 ? 2 : 1), MODE>(a, st) \
-                                : launch_fft_cwt<L, 1, MODE>(a, st);
+#define WTMI_CASE(L) \
+  case L:            \
+    return launch_fft_cwt<L, 1, MODE>(a, st);
   switch (logn) {
     WTMI_CASE(4) WTMI_CASE(5) WTMI_CASE(6) WTMI_CASE(7) WTMI_CASE(8) WTMI_CASE(9)
     WTMI_CASE(10) WTMI_CASE(11) WTMI_CASE(12) WTMI_CASE(13) WTMI_CASE(14)

@@ -26,8 +26,6 @@ struct CwtArgs {
   int nchunks, chunk;
   int prune;             // 2: band-pruned rows + narrowed entry passes (row_code);
                          // 1: band-pruned rows only; 0: full FFTs
-  int diag;              // diagnostics only (WTMI_CWT_DIAG): 1 = skip the inverse FFTs, 2 = skip stores,
-                         // 4 = stores only, 8 = start-up only (tables, load, forward FFT)
 };
 
 constexpr double kPi = 3.14159265358979323846;

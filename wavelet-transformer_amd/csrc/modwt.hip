@@ -482,24 +482,21 @@ __device__ __forceinline__ int syn_level_chain(const float4* __restrict__ V4, co
   return chain_compute<L, M, NG, PAD>(V4, wv, dqlog, hs, fb, tid, vreg);
 }
 
-// MODE 0: W_j copied global -> LDS at the start of each level.
-// MODE 1: as 0, but W_{j-1} is prefetched into registers while level j computes.
-// MODE 2: W_j taps read straight from global memory (L1/L2); LDS holds V only (n floats),
-//         so two workgroups fit per CU and one's loads overlap the other's math.
-// MODE 3: as 2, but levels with a whole-group dilation run along dilation chains
-//         (syn_level_chain: each W_j / V_j tap loaded ~2x instead of 8x).
-// MODE 6: as 3, and a chain level's W taps are loaded at the end of the level before
-//         (after its math, before its barrier and V write), so their latency overlaps the
-//         barrier wait, the V exchange and the V tap reads.
-// MODE 7: as 6 for the first 8 of the M+L-1 taps (register budget).
+// MODE 0: W_j copied global -> LDS at the start of each level (rows of <= 8192 samples).
+// MODE 3: W_j taps read straight from global memory (L1/L2); LDS holds V only (padded, n
+//         floats), so two workgroups fit per CU and one's loads overlap the other's math;
+//         levels with a whole-group dilation run along dilation chains (syn_level_chain:
+//         each W_j / V_j tap loaded ~2x instead of 8x).
+// (r01 also measured: W_{j-1} prefetched into registers during level j, W via LDS with
+// chains, and chain taps loaded one level ahead -- all slower or spilling at the 128-VGPR
+// budget of two workgroups per CU)
 template <int L, int GROUPS, int T, int MODE>
-__global__ void __launch_bounds__(T, MODE >= 6 ? 4 : 1)  // MODE 6/7: <= 128 VGPRs (2 workgroups per CU)
+__global__ void __launch_bounds__(T, 1)
     imodwt_vec_kernel(const float* __restrict__ w, int n, int level, FilterBank fb, unsigned long long keep,
                       float* __restrict__ x, long long ld_out) {
-  constexpr bool PREFETCH = MODE == 1;
-  constexpr bool PAD = MODE >= 2;  // V alone in LDS: padded (vpad), see window_taps
-  constexpr bool CHAINS = MODE == 3 || MODE >= 6;
-  constexpr int PF = MODE == 7 ? 8 : GROUPS + L - 1;  // W taps loaded a level ahead
+  static_assert(MODE == 0 || MODE == 3, "synthesis modes: 0 (W via LDS) or 3 (W global + chains)");
+  constexpr bool PAD = MODE == 3;  // V alone in LDS: padded (vpad), see window_taps
+  constexpr bool CHAINS = MODE == 3;
   constexpr int NG = GROUPS * T;
   constexpr int NGC = (NG & (NG - 1)) == 0 ? NG : 1;
   extern __shared__ __attribute__((aligned(16))) float4 sm4[];
@@ -524,27 +521,11 @@ __global__ void __launch_bounds__(T, MODE >= 6 ? 4 : 1)  // MODE 6/7: <= 128 VGP
     }
     return -1;
   };
-  float4 wpre[GROUPS + L - 1];  // MODE 6: this level's W taps, loaded during the level before
-  bool have = false;
-  float4 pre[GROUPS];
-  if (PREFETCH) {
-    const float4* wr = reinterpret_cast<const float4*>(win + static_cast<long long>(level - 1) * n);
-#pragma unroll
-    for (int k = 0; k < GROUPS; ++k) pre[k] = wr[min(tid + k * T, ng - 1)];
-#pragma unroll
-    for (int k = 0; k < GROUPS; ++k)
-      if (tid + k * T < ng) W4[tid + k * T] = pre[k];
-  }
   for (int j = level; j >= 1; --j) {
     const float4* wr = reinterpret_cast<const float4*>(win + static_cast<long long>(j - 1) * n);
     if (MODE == 0)
       for (int q = tid; q < ng; q += T) W4[q] = wr[q];
     __syncthreads();
-    if (PREFETCH && j > 1) {
-      const float4* wn = reinterpret_cast<const float4*>(win + static_cast<long long>(j - 2) * n);
-#pragma unroll
-      for (int k = 0; k < GROUPS; ++k) pre[k] = wn[min(tid + k * T, ng - 1)];
-    }
     const float wsel = ((keep >> (j - 1)) & 1ull) ? 1.f : 0.f;  // masked rows count as 0
     const int dm = dilation_mod(j, n);
     int tl = tid;
@@ -555,36 +536,18 @@ __global__ void __launch_bounds__(T, MODE >= 6 ? 4 : 1)  // MODE 6/7: <= 128 VGP
       float hs[L];
 #pragma unroll
       for (int l = 0; l < L; ++l) hs[l] = wsel * fb.h[l];
-      int q0;
-      if constexpr (MODE >= 6) {
-        if (!have)
-          chain_load_w<L, GROUPS, NGC>(wr, dqlog, tl, wpre);
-        else if constexpr (PF < GROUPS + L - 1)
-          chain_load_w<L, GROUPS, NGC, PF>(wr, dqlog, tl, wpre);
-        q0 = chain_compute<L, GROUPS, NGC, PAD>(V4, wpre, dqlog, hs, fb, tl, vreg);
-        const int dn = j > 1 ? chain_log(dilation_mod(j - 1, n)) : -1;
-        have = dn >= 0;
-        asm volatile("" ::: "memory");  // after the level's math (pinned): wpre is free again
-        if (have)
-          chain_load_w<L, GROUPS, NGC, 0, PF>(reinterpret_cast<const float4*>(win + static_cast<long long>(j - 2) * n),
-                                              dn, tl, wpre);
-      } else {
-        q0 = syn_level_chain<L, GROUPS, NGC, PAD>(V4, wr, dqlog, hs, fb, tl, vreg);
-      }
+      const int q0 = syn_level_chain<L, GROUPS, NGC, PAD>(V4, wr, dqlog, hs, fb, tl, vreg);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < GROUPS; ++k) V4[vp(q0 + (k << dqlog))] = vreg[k];
       continue;
     }
-    syn_level<L, GROUPS, T, PAD>(V4, MODE >= 2 ? wr : W4, ng, dm, wsel, fb, tl, vreg);
+    syn_level<L, GROUPS, T, PAD>(V4, MODE == 3 ? wr : W4, ng, dm, wsel, fb, tl, vreg);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < GROUPS; ++k) {
       const int q = tl + k * T;
-      if (q < ng) {
-        V4[vp(q)] = vreg[k];
-        if (PREFETCH && j > 1) W4[q] = pre[k];
-      }
+      if (q < ng) V4[vp(q)] = vreg[k];
     }
   }
   __syncthreads();
@@ -633,8 +596,6 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n_taps == 8 && ni >= 64 && (ni & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 16384) {
-    const char* ev = getenv("WTMI_MODWT_VARIANT");
-    const int var = ev ? atoi(ev) : 0;
     auto launch = [&](auto kernel, int t) {
       allow_lds(kernel, lds);
       hipLaunchKernelGGL(kernel, dim3(batch), dim3(t), lds, st, x, ld, ni, level, fb, w);
@@ -648,15 +609,8 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
       launch(modwt_vec_kernel<8, 1, 1024>, 1024);
     else if (ng <= 2048)
       launch(modwt_vec_kernel<8, 2, 1024>, 1024);
-    else if (var == 1)
-      launch(modwt_vec_kernel<8, 4, 1024>, 1024);
-    else if (var == 2)
-      launch(modwt_vec_kernel<8, 8, 512, 1>, 512);
-    else if (var == 5)
-      launch(modwt_vec_kernel<8, 8, 512, 8>, 512);
-    else if (var == 6)
-      launch(modwt_vec_kernel<8, 8, 512>, 512);  // stride form for every level
-    else  // one-process A/B on two boxes (ms): stride 1.248 / 1.264, chains from dq 8 1.200 / 1.264, from dq 16 1.200 / 1.267
+    else  // chains from dq >= 16 groups; one-process A/B on two boxes (ms): stride form 1.248 /
+          // 1.264, chains from dq 8 1.200 / 1.264, from dq 16 1.200 / 1.267 (r01)
       launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
   } else if (n_taps == 8) {
     allow_lds(modwt_kernel<8>, lds);
@@ -682,8 +636,6 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n_taps == 8 && ni >= 64 && (ni & 3) == 0 && (ld_out & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(w) & 15) == 0 && ni <= 16384) {
-    const char* ev = getenv("WTMI_IMODWT_VARIANT");
-    const int var = ev ? atoi(ev) : 0;
     auto launch = [&](auto kernel, int t) {
       allow_lds(kernel, lds);
       hipLaunchKernelGGL(kernel, dim3(batch), dim3(t), lds, st, w, ni, level, fb, keep_mask, x, ld_out);
@@ -702,19 +654,6 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
       launch(imodwt_vec_kernel<8, 1, 1024, 0>, 1024);
     else if (ng <= 2048)
       launch_lds(imodwt_vec_kernel<8, 2, 1024, 3>, 1024, lds_pad);
-    else if (var == 1)
-      launch(imodwt_vec_kernel<8, 4, 1024, 1>, 1024);
-    else if (var == 2)
-      launch_lds(imodwt_vec_kernel<8, 4, 1024, 2>, 1024, lds_pad);
-    else if (var == 3)
-      launch(imodwt_vec_kernel<8, 4, 1024, 0>, 1024);
-    else if (var == 4)  // C3 A/B (ms): W from global, 2 WG/CU 2.00; W via LDS 2.11; + register prefetch 2.71
-      launch_lds(imodwt_vec_kernel<8, 8, 512, 2>, 512, lds_pad);
-    else if (var == 6)  // all 15 taps a level ahead: 28 VGPRs spilled at the 128 cap, 2.22 ms
-      launch_lds(imodwt_vec_kernel<8, 8, 512, 6>, 512, lds_pad);
-    else if (var == 7)  // one-process A/B (ms): MODE 3 1.506-1.508, MODE 7 1.492-1.495, but
-                        // FETCH_SIZE 6.32 -> 7.15 GB (the early taps fall out of L2 before use)
-      launch_lds(imodwt_vec_kernel<8, 8, 512, 7>, 512, lds_pad);
     else
       launch_lds(imodwt_vec_kernel<8, 8, 512, 3>, 512, lds_pad);
   } else if (n_taps == 8) {

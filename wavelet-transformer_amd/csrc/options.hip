@@ -1,0 +1,67 @@
+// Launch-policy options (common.hpp Options): environment read once, C ABI setter.
+#include <cstdlib>
+#include <cstring>
+
+#include "common.hpp"
+
+namespace wtmi {
+
+namespace {
+struct Entry {
+  const char* name;
+  int Options::*field;
+  int lo, hi;
+};
+constexpr Entry kEntries[] = {
+    {"cwt_prune", &Options::cwt_prune, 0, 2},
+    {"cwt_target_wg", &Options::cwt_target_wg, 0, 1 << 24},
+    {"wct_prune", &Options::wct_prune, 0, 1},
+    {"wct_target_wg", &Options::wct_target_wg, 0, 1 << 24},
+    {"wct_min_rows", &Options::wct_min_rows, 1, 1 << 10},
+};
+
+Options& mutable_options() {
+  static Options opts = [] {
+    Options o;
+    for (const Entry& e : kEntries) {
+      char env[64] = "WTMI_";
+      size_t k = 5;
+      for (const char* c = e.name; *c && k + 1 < sizeof(env); ++c) env[k++] = static_cast<char>(*c >= 'a' && *c <= 'z' ? *c - 32 : *c);
+      env[k] = 0;
+      if (const char* v = getenv(env)) {
+        const long x = strtol(v, nullptr, 10);
+        if (x >= e.lo && x <= e.hi) o.*(e.field) = static_cast<int>(x);
+      }
+    }
+    return o;
+  }();
+  return opts;
+}
+}  // namespace
+
+const Options& options() { return mutable_options(); }
+
+}  // namespace wtmi
+
+// Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
+// wct_min_rows).  0 on success, -1 unknown name or out of range.  Applies to launches
+// issued after the call; not to be called while another thread is launching.
+extern "C" int wtmi_set_option(const char* name, long long value) {
+  if (!name) return wtmi::kErrArg;
+  for (const auto& e : wtmi::kEntries) {
+    if (strcmp(name, e.name) == 0) {
+      if (value < e.lo || value > e.hi) return wtmi::kErrArg;
+      wtmi::mutable_options().*(e.field) = static_cast<int>(value);
+      return wtmi::kOk;
+    }
+  }
+  return wtmi::kErrArg;
+}
+
+// Current value of an option, or -1 for an unknown name.
+extern "C" long long wtmi_get_option(const char* name) {
+  if (!name) return -1;
+  for (const auto& e : wtmi::kEntries)
+    if (strcmp(name, e.name) == 0) return wtmi::options().*(e.field);
+  return -1;
+}

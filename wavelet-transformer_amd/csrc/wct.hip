@@ -764,15 +764,13 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int*
     if (rc != kOk) return rc;
   }
   const int rows = G::ROWS;
-  const char* ev = getenv("WTMI_WCT_TARGET_WG");
   // Row costs differ a lot (full-band rows several transforms, band rows few): more,
   // shorter workgroups balance better.  C4 ms (one box, two alternations): target 2048
   // 5.10, 4096 4.53-4.58, 8192 4.11-4.23, 12800 (= 4 rows each) 4.08-4.11; 4 rows each
   // 3.95-4.09 vs 3 rows 4.01-4.09, 2 rows 4.03-4.13.  Default: 4-row workgroups.
-  const long long target = ev ? atoll(ev) : (1ll << 30);
+  const long long target = options().wct_target_wg > 0 ? options().wct_target_wg : (1ll << 30);
   long long want = (target + a.batch - 1) / a.batch;
-  const char* mr = getenv("WTMI_WCT_MIN_ROWS");
-  const int min_rows = mr && atoi(mr) > 0 ? atoi(mr) : 4;  // rows per workgroup, at least
+  const int min_rows = options().wct_min_rows;  // rows per workgroup, at least
   const int max_chunks = (a.S + min_rows * rows - 1) / (min_rows * rows);
   int nch = static_cast<int>(want < 1 ? 1 : want);
   if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
@@ -782,8 +780,7 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int*
   nch = (a.S + chunk - 1) / chunk;
   a.nchunks = nch;
   a.chunk = chunk;
-  const char* pe = getenv("WTMI_WCT_PRUNE");
-  a.prune = pe ? atoi(pe) : 1;
+  a.prune = options().wct_prune;
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
   hipLaunchKernelGGL(wct_plan_kernel<LOGN>, dim3(1), dim3(256), 0, st, a.scales, a.S, a.dt, a.f0, K,
@@ -806,20 +803,13 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int*
 template <int K>
 static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0, int S, float* coh,
                           const int* plan, hipStream_t st) {
-  // one column per thread by default (twice the threads, more loads in flight: C4 4.73 ->
-  // 4.65 ms); WTMI_WCT_B_COLS=2: 16-byte column pairs (even rows)
-  const char* ec = getenv("WTMI_WCT_B_COLS");
-  const bool pairs = (n0 % 2) == 0 && ec && atoi(ec) == 2;
-  const long long ncol = pairs ? n0 / 2 : n0;
-  const long long tiles = (ncol + 255) / 256;
+  // one column per thread (16-byte column pairs measured slower: fewer loads in flight,
+  // C4 4.65 vs 4.73 ms in r01)
+  const long long tiles = (static_cast<long long>(n0) + 255) / 256;
   const long long grid = batch * tiles;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  if (pairs)
-    hipLaunchKernelGGL((wct_phase_b<K, 2>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
-                       batch, n0, S, coh, plan);
-  else
-    hipLaunchKernelGGL((wct_phase_b<K, 1>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
-                       batch, n0, S, coh, plan);
+  hipLaunchKernelGGL((wct_phase_b<K, 1>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
+                     batch, n0, S, coh, plan);
   return launch_status();
 }
 

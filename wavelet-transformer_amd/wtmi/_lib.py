@@ -39,6 +39,8 @@ PROTOTYPES = {
     "wtmi_waverec": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _P]),
     "wtmi_series_moments": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P]),
     "wtmi_affine": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I64, _P]),
+    "wtmi_set_option": (_I32, [C.c_char_p, _I64]),
+    "wtmi_get_option": (_I64, [C.c_char_p]),
 }
 
 ERRORS = {-1: "invalid argument", -2: "unsupported size"}
@@ -69,6 +71,35 @@ def load() -> C.CDLL:
                 fn.argtypes = args
             _lib = lib
     return _lib
+
+
+def set_option(name: str, value: int) -> int:
+    """Set a launch option (include/wtmi.h); returns the previous value."""
+    old = get_option(name)
+    call("wtmi_set_option", name.encode(), int(value))
+    return old
+
+
+def get_option(name: str) -> int:
+    v = load().wtmi_get_option(name.encode())
+    if v < 0:
+        raise WtmiError(f"unknown option {name!r}")
+    return int(v)
+
+
+class option:
+    """Context manager: ``with _lib.option("cwt_prune", 0): ...`` (tests / A/B scripts)."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.old = set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.name, self.old)
+        return False
 
 
 def call(name: str, *args) -> int:
