@@ -32,14 +32,16 @@ extern "C" {
  * x: [batch][ld] float32, n0 <= 16384 samples used per series.
  * affine: optional [batch][3] float64 (a0, a1, a2): x' = (x - a0 - a1*t) * a2 applied
  *         before the transform (standardize_series / pycwt normalisation), or NULL.
- * scales: [n_scales] float64 (s_j).  sig_scale: [n_scales] float64 = 1/signif_j, or
+ * scales: [n_scales] float64 (s_j).  sig_scale: float64 1/signif_j, series b reading
+ *         sig_scale[b * sig_ld + j] (sig_ld = 0: one [n_scales] row for every series,
+ *         else >= n_scales: per-series AR(1) levels, one launch for a whole batch), or
  *         NULL when out_sig is NULL.
  * Outputs (any may be NULL, not all): out_w [batch][n_scales][n0] complex64,
  *         out_power / out_sig [batch][n_scales][n0] float32.                       */
 int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
                     const double* affine, const double* scales, int n_scales, double dt,
-                    double f0, const double* sig_scale, float* out_w, float* out_power,
-                    float* out_sig, void* stream);
+                    double f0, const double* sig_scale, long long sig_ld, float* out_w,
+                    float* out_power, float* out_sig, void* stream);
 
 /* ---- XWT / phase (K1+K2, pair mode) ------------------------------------------
  * Replaces the two pycwt.cwt calls and W1*conj(W2) inside pycwt.xwt
@@ -50,8 +52,8 @@ int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
 int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long batch,
                     long long n0, const double* affine1, const double* affine2,
                     const double* scales, int n_scales, double dt, double f0,
-                    const double* sig_scale, float* out_w12, float* out_power, float* out_sig,
-                    float* out_u, float* out_v, void* stream);
+                    const double* sig_scale, long long sig_ld, float* out_w12, float* out_power,
+                    float* out_sig, float* out_u, float* out_v, void* stream);
 
 /* ---- WCT coherence + XWT power / phase (K1+K2+K7+K8) ---------------------------
  * Replaces pycwt.wct(..., sig=False) numerics (src/wct.py:106-118): two CWTs,

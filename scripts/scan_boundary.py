@@ -8,8 +8,9 @@ or executed from it):
 Two things are recorded, both as plain data (names, parameter kinds, default-value
 expressions, file:line of each use):
 
-* ``surface``: the public top-level names of the six modules the engine replaces --
-  src/{cwt,xwt,wct,dwt,modwt}.py and src/utils/wavelet_helpers.py -- with the signature of
+* ``surface``: the public top-level names of the seven modules the engine replaces --
+  src/{cwt,xwt,wct,dwt,modwt}.py, src/utils/wavelet_helpers.py and
+  src/utils/transform_helpers.py (the batch API) -- with the signature of
   every function, every dataclass's generated ``__init__`` and every method, and the
   value expression of every module constant.
 * ``uses``: every attribute of those modules that the reference's callers touch
@@ -37,9 +38,11 @@ MODULES = {
     "dwt": "src/dwt.py",
     "modwt": "src/modwt.py",
     "wavelet_helpers": "src/utils/wavelet_helpers.py",
+    "transform_helpers": "src/utils/transform_helpers.py",
 }
 DOTTED = {"src." + k: k for k in ("cwt", "xwt", "wct", "dwt", "modwt")}
 DOTTED["src.utils.wavelet_helpers"] = "wavelet_helpers"
+DOTTED["src.utils.transform_helpers"] = "transform_helpers"
 
 # Names that are not part of the replaced API: script entry points, loggers and the
 # module-level config the reference's own __main__ blocks use.

@@ -6,7 +6,7 @@ src/{cwt,xwt,wct,dwt,modwt}.py and src/utils/wavelet_helpers.py, and every attri
 those modules the reference's callers use (app/, src/, tests/), with file:line.  Here the
 repo's modules must expose every such name with an identical parameter list (names,
 kinds, defaults), constants with equal values, and the overlay must replace exactly those
-six modules inside an otherwise untouched reference-shaped ``src`` tree.
+seven modules inside an otherwise untouched reference-shaped ``src`` tree.
 """
 
 import ast
@@ -26,7 +26,8 @@ with open(os.path.join(GOLDEN, "boundary_attrs.json")) as _fh:
     BOUNDARY = json.load(_fh)
 
 MODNAMES = {"cwt": "src.cwt", "xwt": "src.xwt", "wct": "src.wct", "dwt": "src.dwt",
-            "modwt": "src.modwt", "wavelet_helpers": "src.utils.wavelet_helpers"}
+            "modwt": "src.modwt", "wavelet_helpers": "src.utils.wavelet_helpers",
+            "transform_helpers": "src.utils.transform_helpers"}
 # Constants whose reference value is a third-party object (pycwt / pywt instances): the
 # name must exist; what it holds is checked by test_mother_wavelet_constants.
 OBJECT_CONSTANTS = {"MOTHER", "MOTHER_DICT"}
@@ -175,18 +176,17 @@ FAKE_REF = {
     "src/retrieve_data.py": "WHO = 'reference'\n",
     # src/utils has no __init__.py in the reference (a namespace package)
     "src/utils/wavelet_helpers.py": "raise ImportError('reference wavelet_helpers imported')\n",
+    "src/utils/transform_helpers.py": "raise ImportError('reference transform_helpers imported')\n",
     "src/utils/helpers.py": "WHO = 'reference'\n",
-    "src/utils/transform_helpers.py": textwrap.dedent("""\
-        from src import cwt, dwt, xwt
-        from src.cwt import DataForCWT, ResultsFromCWT
-        from src.dwt import DataForDWT, ResultsFromDWT
-        from src.utils import wavelet_helpers
-        from src.xwt import DataForXWT, ResultsFromXWT
+    "src/regression.py": textwrap.dedent("""\
+        from src.utils.transform_helpers import create_dwt_dict, create_dwt_results_dict
+        from src import dwt, retrieve_data
+        from src.utils.wavelet_helpers import align_series
         """),
     "src/wavelet_plots.py": textwrap.dedent("""\
         from src import cwt, dwt, wct, xwt
         from src.utils.helpers import WHO
-        from src.utils.transform_helpers import DataForCWT
+        from src.utils.transform_helpers import DataForCWT, create_cwt_results_dict
         from src.utils.wavelet_helpers import standardize_series
         """),
 }
@@ -198,10 +198,11 @@ PROBE = textwrap.dedent("""\
     from src import retrieve_data, modwt
     from src.utils import helpers, wavelet_helpers
     import src.utils.transform_helpers as th
+    import src.regression
     out = {{m: sys.modules[m].__file__ for m in
            ["src", "src.cwt", "src.xwt", "src.wct", "src.dwt", "src.modwt",
             "src.utils.wavelet_helpers", "src.utils.helpers", "src.retrieve_data",
-            "src.wavelet_plots", "src.utils.transform_helpers"]}}
+            "src.wavelet_plots", "src.utils.transform_helpers", "src.regression"]}}
     out["plot_cwt"] = hasattr(wp.cwt, "plot_cwt")
     out["utils_is_namespace"] = getattr(sys.modules["src.utils"], "__file__", None) is None
     print(json.dumps(out))
@@ -229,10 +230,10 @@ def _probe(ref, activate, extra_path=()):
 
 def _assert_overlaid(out, ref):
     ours = os.path.realpath(os.path.join(PKG, "src"))
-    for m in ("src.cwt", "src.xwt", "src.wct", "src.dwt", "src.modwt", "src.utils.wavelet_helpers"):
-        assert os.path.realpath(out[m]).startswith(ours + os.sep), (m, out[m])
-    for m in ("src", "src.utils.helpers", "src.retrieve_data", "src.wavelet_plots",
+    for m in ("src.cwt", "src.xwt", "src.wct", "src.dwt", "src.modwt", "src.utils.wavelet_helpers",
               "src.utils.transform_helpers"):
+        assert os.path.realpath(out[m]).startswith(ours + os.sep), (m, out[m])
+    for m in ("src", "src.utils.helpers", "src.retrieve_data", "src.wavelet_plots", "src.regression"):
         assert os.path.realpath(out[m]).startswith(os.path.realpath(ref) + os.sep), (m, out[m])
     assert out["plot_cwt"] and out["utils_is_namespace"]
 
@@ -266,7 +267,7 @@ def test_overlay_stub_files_and_restore(tmp_path):
     ref = str(tmp_path / "reference")
     _fake_reference(ref)
     written = overlay.write_stubs(ref)
-    assert len(written) == 6
+    assert len(written) == 7
     overlay.write_stubs(ref)  # idempotent: the originals stay in *.orig
     out = _probe(ref, "sys.path.insert(0, '.')")
     # with stubs the modules live at the reference's paths but run the engine's code

@@ -41,8 +41,8 @@ def test_prototype_arity_matches_header():
 def test_invalid_arguments_rejected_without_gpu():
     from wtmi import _lib
     lib = _lib.load()
-    assert lib.wtmi_cwt_morlet(None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, None, None, None,
-                               None) == -1
+    assert lib.wtmi_cwt_morlet(None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, 0, None, None,
+                               None, None) == -1
     assert lib.wtmi_modwt(None, 16, 1, 16, None, None, 8, 2, None, None) == -1
     assert lib.wtmi_wavedec(None, 16, 1, 16, None, None, 8, 2, None, None) == -1
     assert lib.wtmi_series_moments(None, 0, 1, 1, 1, None, None) == -1

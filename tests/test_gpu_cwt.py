@@ -139,7 +139,7 @@ def test_rejects_cpu_tensors_and_bad_args():
         ops.cwt_morlet(torch.zeros(1, 16), [1.0], 1.0)
     from wtmi import _lib
     with pytest.raises(_lib.WtmiError):
-        _lib.call("wtmi_cwt_morlet", None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, None, None,
+        _lib.call("wtmi_cwt_morlet", None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, 0, None, None,
                   None, None)
 
 
@@ -161,3 +161,39 @@ def test_torch_custom_ops_match_oracle(db4):
     assert np.abs(w[0].cpu().numpy() - r).max() <= 1e-5 * np.abs(r).max()
     xr = torch.ops.wtmi.imodwt(w, lo, hi).cpu().numpy()
     assert np.abs(xr - x).max() <= 1e-5 * np.abs(x).max()
+
+
+def test_torch_custom_ops_xwt_dwt_stats(db4):
+    """torch.ops.wtmi.{xwt, xwt_power, dwt, idwt, series_stats} vs the oracle, and their
+    fake (meta) kernels agree with the real output shapes."""
+    import wtmi.ops  # noqa: F401
+    from oracle import dwt_spec as ds
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    rng = np.random.default_rng(22)
+    n0, dt, dj, J = 700, 1 / 12, 1 / 8, 50
+    x1 = np.stack([red_series(rng, n0) for _ in range(2)])
+    x2 = np.stack([red_series(rng, n0) for _ in range(2)])
+    sj = torch.tensor(_scales(n0, dt, dj, 2 * dt, J), device="cuda")
+    d1, d2 = torch.tensor(x1, device="cuda"), torch.tensor(x2, device="cuda")
+    W12 = torch.ops.wtmi.xwt(d1, d2, sj, dt, 6.0)
+    P = torch.ops.wtmi.xwt_power(d1, d2, sj, dt, 6.0)
+    ref = (pc.cwt(x1[1].astype(np.float64), dt, dj, 2 * dt, J)[0]
+           * pc.cwt(x2[1].astype(np.float64), dt, dj, 2 * dt, J)[0].conj())
+    assert row_relerr(W12[1].cpu().numpy().astype(np.complex128), ref).max() < 5e-5
+    assert row_relerr(P[1].cpu().numpy().astype(np.float64), np.abs(ref) ** 2).max() < 5e-5
+    lo, hi = torch.tensor(db4["dec_lo"]), torch.tensor(db4["dec_hi"])
+    rlo, rhi = torch.tensor(db4["rec_lo"]), torch.tensor(db4["rec_hi"])
+    C = torch.ops.wtmi.dwt(d1, lo, hi, 5)
+    flat = np.concatenate(ds.wavedec(x1[0].astype(np.float64), db4["dec_lo"], db4["dec_hi"], 5))
+    assert C.shape[1] == flat.size and np.abs(C[0].cpu().numpy() - flat).max() <= 1e-5 * np.abs(flat).max()
+    back = torch.ops.wtmi.idwt(C, n0, rlo, rhi, 5).cpu().numpy()
+    assert back.shape == (2, n0) and np.abs(back - x1).max() <= 1e-5 * np.abs(x1).max()
+    st = torch.ops.wtmi.series_stats(d1).cpu().numpy()
+    np.testing.assert_allclose(st[:, 0], x1.astype(np.float64).mean(axis=1), rtol=1e-9)
+    np.testing.assert_allclose(st[:, 1], x1.astype(np.float64).std(axis=1), rtol=1e-9)
+    with FakeTensorMode():
+        f1 = torch.empty(2, n0, device="cuda")
+        fs = torch.empty(sj.numel(), dtype=torch.float64, device="cuda")
+        assert torch.ops.wtmi.xwt(f1, f1, fs, dt, 6.0).shape == W12.shape
+        assert torch.ops.wtmi.dwt(f1, lo, hi, 5).shape == C.shape
+        assert torch.ops.wtmi.series_stats(f1).shape == (2, 8)

@@ -56,3 +56,40 @@ def test_oracle_rednoise_is_ar1():
     r1 = np.corrcoef(x[:-1], x[1:])[0, 1]
     assert abs(r1 - 0.7) < 0.01
     assert abs(x.var() - 1 / (1 - 0.49)) < 0.05
+
+
+def test_quantile_known_answer_with_empty_bins_at_the_crossing():
+    """Hand-built counter: 10 counts in bin 0, bins 1-4 EMPTY, 10 counts in bin 5 (nbins 10).
+    The selection rule interpolates over non-empty bins only: P = ((10, 20) - 0.5) / 20 =
+    (0.475, 0.975) on the mid-bin grid (0.05, 0.55), so the 95 % level is
+    0.05 + (0.95 - 0.475) / 0.5 * 0.5 = 0.525.  (Parity unpinned: the rule restates pycwt's
+    masked-array selection; no reference fixture exists for this step.)"""
+    from wtmi import transforms
+    wlc = np.zeros((2, 10))
+    wlc[0, 0] = wlc[0, 5] = 10
+    got = transforms.significance_from_histogram(wlc, np.array([True, True]), 1, 0.95)
+    assert got[0] == pytest.approx(0.525, abs=1e-15)
+    assert np.isnan(got[1])
+    ref = pc.significance_from_histogram(wlc, np.ones((2, 4), dtype=bool), 1, 0.95)
+    assert ref[0] == pytest.approx(0.525, abs=1e-15)
+
+
+def test_significance_cache_persists_on_disk(tmp_path, monkeypatch):
+    """wct_significance(cache=True) keeps results in memory AND on disk (pycwt's cache=True,
+    src/wct.py:117): a fresh process (empty memory cache) reads the stored levels back."""
+    from wtmi import transforms
+    monkeypatch.setenv("WTMI_CACHE_DIR", str(tmp_path))
+    key = ("wct_significance", 1, 0.7, 0.5, 1 / 12, 0.125, 2 / 12, 40, 0.95, 6.0, 300, 1000, None)
+    assert transforms.sig_cache_load(key) is None
+    sig = np.linspace(0.1, 0.9, 41)
+    sig[-3:] = np.nan
+    transforms.sig_cache_store(key, sig)
+    monkeypatch.setattr(transforms, "_sig_cache", {})
+    back = transforms.sig_cache_load(key)
+    np.testing.assert_array_equal(back, sig)
+    files = list((tmp_path / "wct_sig").iterdir())
+    assert len(files) == 1 and files[0].suffix == ".npy"
+    # an unreadable entry is recomputed, never trusted
+    files[0].write_bytes(b"garbage")
+    monkeypatch.setattr(transforms, "_sig_cache", {})
+    assert transforms.sig_cache_load(key) is None

@@ -157,7 +157,7 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const double s = a.scales[j0 + i];
     const cpx mp = morlet_params(s, a.dt, P::N);
-    const float sg = a.sigscale ? static_cast<float>(a.sigscale[j0 + i]) : 0.f;
+    const float sg = a.sigscale ? static_cast<float>(a.sigscale[b * a.sig_ld + j0 + i]) : 0.f;
     const int code = NBUF == 1 ? row_code<LOGN>(s, a.dt, a.f0, a.prune) : 0;
     prm_tab[i] = make_float4(mp.x, mp.y, sg, static_cast<float>(code));
   }
@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(256) cwt_direct_kernel(CwtArgs a, int N) {
   if (a.out_w) a.out_w[o] = v;
   const float pw = cabs2(v);
   if (a.out_pow) a.out_pow[o] = pw;
-  if (a.out_sig) a.out_sig[o] = pw * static_cast<float>(a.sigscale[j]);
+  if (a.out_sig) a.out_sig[o] = pw * static_cast<float>(a.sigscale[b * a.sig_ld + j]);
   if constexpr (MODE == 1) {
     if (a.out_u) {
       const float r = sqrtf(pw);
@@ -352,9 +352,10 @@ using namespace wtmi;
 
 extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
                                const double* affine, const double* scales, int n_scales,
-                               double dt, double f0, const double* sig_scale, float* out_w,
-                               float* out_power, float* out_sig, void* stream) {
+                               double dt, double f0, const double* sig_scale, long long sig_ld,
+                               float* out_w, float* out_power, float* out_sig, void* stream) {
   if (!x || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
+  if (sig_ld != 0 && sig_ld < n_scales) return kErrArg;
   if (!out_w && !out_power && !out_sig) return kErrArg;
   if (out_sig && !sig_scale) return kErrArg;
   if (n0 > (1 << 14)) return kErrUnsupported;
@@ -369,6 +370,7 @@ extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, lo
   a.dt = dt;
   a.f0 = f0;
   a.sigscale = sig_scale;
+  a.sig_ld = sig_ld;
   a.out_w = reinterpret_cast<cpx*>(out_w);
   a.out_pow = out_power;
   a.out_sig = out_sig;
@@ -378,9 +380,11 @@ extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, lo
 extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long batch,
                                long long n0, const double* affine1, const double* affine2,
                                const double* scales, int n_scales, double dt, double f0,
-                               const double* sig_scale, float* out_w12, float* out_power,
-                               float* out_sig, float* out_u, float* out_v, void* stream) {
+                               const double* sig_scale, long long sig_ld, float* out_w12,
+                               float* out_power, float* out_sig, float* out_u, float* out_v,
+                               void* stream) {
   if (!x1 || !x2 || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
+  if (sig_ld != 0 && sig_ld < n_scales) return kErrArg;
   if (!out_w12 && !out_power && !out_sig && !out_u) return kErrArg;
   if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
   if (out_sig && !sig_scale) return kErrArg;
@@ -398,6 +402,7 @@ extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, l
   a.dt = dt;
   a.f0 = f0;
   a.sigscale = sig_scale;
+  a.sig_ld = sig_ld;
   a.out_w = reinterpret_cast<cpx*>(out_w12);
   a.out_pow = out_power;
   a.out_sig = out_sig;

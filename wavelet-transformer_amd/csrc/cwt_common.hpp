@@ -17,7 +17,9 @@ struct CwtArgs {
   const double* affine2;
   const double* scales;  // [S] device
   double dt, f0;
-  const double* sigscale;  // [S] multiplier for the ratio output (1 / signif), or null
+  const double* sigscale;  // [S] multiplier for the ratio output (1 / signif), or null;
+                           // series b uses sigscale + b * sig_ld (sig_ld 0: one row for all)
+  long long sig_ld;
   cpx* out_w;
   float* out_pow;
   float* out_sig;

@@ -74,33 +74,56 @@ def run_cwt(cwt_data: Type[DataForCWT], normalize: bool = True, standardize: boo
             **kwargs) -> Type[ResultsFromCWT]:
     """Conducts Continuous Wavelet Transform.
     Returns power spectrum, period, cone of influence, and significance levels."""
-    mother = as_morlet(cwt_data.mother_wavelet)
-    y = transforms._to_dev(np.asarray(cwt_data.y_values)).reshape(1, -1)
-    mom_y = ops.series_moments(y)
-    if standardize:
-        # kwargs go to standardize_series as in the reference (:102): an unknown keyword
-        # raises TypeError there and here
-        coef = transforms.standardize_coefs(mom_y, **kwargs)
-        x32 = ops.affine(y, coef, torch.float32)
-    else:  # quirk B.1: `normalize` has no effect
-        x32 = ops.affine(y, torch.tensor([[0.0, 0.0, 1.0]], dtype=torch.float64, device=y.device),
-                         torch.float32)
-    m = transforms._np(mom_y)[0]
-    alpha, _, _ = transforms._ar1_from_moments(m[4], m[5], int(m[6]))  # quirk B.2
+    return run_cwt_batch([cwt_data], normalize=normalize, standardize=standardize,
+                         calculate_significance=calculate_significance,
+                         significance_level=significance_level, **kwargs)[0]
 
-    n0 = y.shape[1]
-    sj, freqs = transforms.scales_for(n0, DT, DJ, S0, J, mother)
-    sig_scale = None
-    if calculate_significance:
-        signif, _ = transforms.significance(1.0, DT, sj, 0, alpha,
-                                            significance_level=significance_level, wavelet=mother)
-        sig_scale = 1.0 / signif
-    res = ops.cwt_morlet(x32, sj, DT, mother.f0, sig_scale=sig_scale, want_w=False,
-                         want_power=True, want_sig=calculate_significance)
-    power = transforms._np(res["power"][0], np.float64)
-    sig = transforms._np(res["sig"][0], np.float64) if calculate_significance else None
-    coi = transforms.cone_of_influence(n0, DT, mother)
-    return ResultsFromCWT(power, 1 / freqs, sig, coi)
+
+def run_cwt_batch(cwt_data_list: List[DataForCWT], normalize: bool = True,
+                  standardize: bool = False, calculate_significance: bool = True,
+                  significance_level: float = 0.95, **kwargs) -> List[ResultsFromCWT]:
+    """``run_cwt`` over many series (engine extension; the reference loops in
+    src/utils/transform_helpers.py:116-123).  Series of one length and mother wavelet
+    share one moments launch, one affine launch and ONE fused CWT launch; each keeps its
+    own AR(1) significance (a [B, S] multiplier).  Results are those of run_cwt per series."""
+    out: List[ResultsFromCWT] = [None] * len(cwt_data_list)
+    groups: dict = {}
+    for i, d in enumerate(cwt_data_list):
+        mother = as_morlet(d.mother_wavelet)
+        groups.setdefault((np.asarray(d.y_values).size, mother.f0), []).append(i)
+    for (n0, f0), idx in groups.items():
+        mother = as_morlet(cwt_data_list[idx[0]].mother_wavelet)
+        y = transforms._to_dev(np.stack([np.asarray(cwt_data_list[i].y_values, dtype=np.float64)
+                                         for i in idx]))
+        mom_y = ops.series_moments(y)
+        if standardize:
+            # kwargs go to standardize_series as in the reference (:102): an unknown keyword
+            # raises TypeError there and here
+            coef = transforms.standardize_coefs(mom_y, **kwargs)
+        else:  # quirk B.1: `normalize` has no effect
+            coef = torch.zeros((len(idx), 3), dtype=torch.float64, device=y.device)
+            coef[:, 2] = 1.0
+        x32 = ops.affine(y, coef, torch.float32)
+        m = transforms._np(mom_y)
+        sj, freqs = transforms.scales_for(n0, DT, DJ, S0, J, mother)
+        sig_scale = None
+        if calculate_significance:
+            rows = []
+            for k in range(len(idx)):  # quirk B.2: AR(1) of y_values, not the standardised series
+                alpha, _, _ = transforms._ar1_from_moments(m[k, 4], m[k, 5], int(m[k, 6]))
+                signif, _ = transforms.significance(1.0, DT, sj, 0, alpha,
+                                                    significance_level=significance_level,
+                                                    wavelet=mother)
+                rows.append(1.0 / signif)
+            sig_scale = np.stack(rows)
+        res = ops.cwt_morlet(x32, sj, DT, mother.f0, sig_scale=sig_scale, want_w=False,
+                             want_power=True, want_sig=calculate_significance)
+        power = transforms._np(res["power"], np.float64)
+        sig = transforms._np(res["sig"], np.float64) if calculate_significance else None
+        coi = transforms.cone_of_influence(n0, DT, mother)
+        for k, i in enumerate(idx):
+            out[i] = ResultsFromCWT(power[k], 1 / freqs, None if sig is None else sig[k], coi.copy())
+    return out
 
 
 def plot_cwt(cwt_ax, cwt_data: Type[DataForCWT], cwt_results: Type[ResultsFromCWT],

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import logging
 from dataclasses import dataclass, field
-from typing import Dict, Type
+from typing import Dict, List, Type
 
 import numpy as np
 import numpy.typing as npt
@@ -76,15 +76,40 @@ def trim_signal(original_signal: npt.NDArray, reconstructed: npt.NDArray) -> npt
 
 def run_dwt(dwt_data: Type[DataForDWT]) -> Type[ResultsFromDWT]:
     """Coefficients from a pyramid DWT; ``levels=None`` means pywt's maximum level."""
-    w = as_filter_bank(dwt_data.mother_wavelet)
-    if dwt_data.levels is None:
-        dwt_levels = transforms.dwt_max_level(len(dwt_data.y_values), w.dec_len)
-        print(f"""Max decomposition level of {dwt_levels} for time series length
-            of {len(dwt_data.y_values)}""")
-    else:
-        dwt_levels = dwt_data.levels
-    coeffs = transforms.wavedec(dwt_data.y_values, w, level=dwt_data.levels)
-    return ResultsFromDWT(coeffs, dwt_levels)
+    return run_dwt_batch([dwt_data])[0]
+
+
+def run_dwt_batch(dwt_data_list: List[DataForDWT]) -> List[ResultsFromDWT]:
+    """``run_dwt`` over many series (engine extension; the reference loops in
+    src/utils/transform_helpers.py:89-113): series of one length, wavelet and level share
+    ONE analysis launch."""
+    out = []
+    for d, coeffs in zip(dwt_data_list, wavedec_batch(dwt_data_list)):
+        if d.levels is None:
+            dwt_levels = transforms.dwt_max_level(len(d.y_values),
+                                                  as_filter_bank(d.mother_wavelet).dec_len)
+            print(f"""Max decomposition level of {dwt_levels} for time series length
+            of {len(d.y_values)}""")
+        else:
+            dwt_levels = d.levels
+        out.append(ResultsFromDWT(coeffs, dwt_levels))
+    return out
+
+
+def wavedec_batch(dwt_data_list: List[DataForDWT]) -> list:
+    """Coefficient lists of pywt.wavedec(y_values, mother_wavelet, level=levels) for each
+    entry, one launch per group of equal (length, wavelet, level)."""
+    out: list = [None] * len(dwt_data_list)
+    groups: dict = {}
+    for i, d in enumerate(dwt_data_list):
+        w = as_filter_bank(d.mother_wavelet)
+        groups.setdefault((len(d.y_values), w.name, tuple(w.dec_lo), d.levels), []).append(i)
+    for (_, _, _, level), idx in groups.items():
+        w = as_filter_bank(dwt_data_list[idx[0]].mother_wavelet)
+        rows = np.stack([np.asarray(dwt_data_list[i].y_values, dtype=np.float64) for i in idx])
+        for k, c in zip(idx, transforms.wavedec_batch(rows, w, level=level)):
+            out[k] = c
+    return out
 
 
 def reconstruct_signal_component(signal_coeffs: list, wavelet: str, level: int):

@@ -74,51 +74,71 @@ class ResultsFromXWT:
     phase_diff_v: npt.NDArray
 
 
-def _pair(y1, y2):
-    d1 = transforms._to_dev(np.asarray(y1)).reshape(1, -1)
-    d2 = transforms._to_dev(np.asarray(y2)).reshape(1, -1)
-    m1, m2 = ops.series_moments(d1), ops.series_moments(d2)
-    return d1, d2, m1, m2
-
-
 def run_xwt(cross_wavelet_transform: Type[DataForXWT], normalize: bool = True
             ) -> Type[ResultsFromXWT]:
     """Cross-wavelet power, period, significance ratio, COI polygon and phase arrows."""
-    d = cross_wavelet_transform
-    mother = as_morlet(d.mother_wavelet)
-    y1, y2 = np.asarray(d.y1_values), np.asarray(d.y2_values)
-    d1, d2, m1, m2 = _pair(y1, y2)
-    n0 = d1.shape[1]
-    # pycwt.xwt(normalize=True): (y - mean) / std, in fp64 on the GPU
-    x1 = ops.affine(d1, transforms.normalize_coefs(m1), torch.float32)
-    x2 = ops.affine(d2, transforms.normalize_coefs(m2), torch.float32)
-    sj, freqs = transforms.scales_for(n0, d.delta_t, d.delta_j, d.initial_scale, -1, mother)
-    mh1, mh2 = transforms._np(m1)[0], transforms._np(m2)[0]
-    g1, _, _ = transforms._ar1_from_moments(mh1[4], mh1[5], int(mh1[6]))
-    g2, _, _ = transforms._ar1_from_moments(mh2[4], mh2[5], int(mh2[6]))
-    Pk1 = transforms.ar1_spectrum(freqs * d.delta_t, g1)
-    Pk2 = transforms.ar1_spectrum(freqs * d.delta_t, g2)
-    dof = mother.dofmin
-    signif = (Pk1 * Pk2) ** 0.5 * transforms._chi2_ppf(0.95, dof) / dof  # std1 = std2 = 1
-    period = 1 / freqs
-    coi = transforms.cone_of_influence(n0, d.delta_t, mother)
-    if normalize:
-        r = ops.xwt_morlet(x1, x2, sj, d.delta_t, mother.f0, sig_scale=1.0 / signif,
-                           want_power=True, want_sig=True)
-        power = transforms._np(r["power"][0], np.float64)
-        sig95 = transforms._np(r["sig"][0], np.float64)
-        coi_plot = coi_polygon(coi, period, np.log2(d.levels[2]))
-    else:
-        r = ops.xwt_morlet(x1, x2, sj, d.delta_t, mother.f0, want_w12=True)
-        power = transforms._np(r["w12"][0], np.complex128)
-        sig95 = power / (np.ones([1, n0]) * signif[:, None])
-        coi_plot = coi
-    # phase: pycwt.wct(..., delta_j=...) runs at its default dj = 1/12 (quirk B.5)
-    sj_p, _ = transforms.scales_for(n0, d.delta_t, 1 / 12, d.initial_scale, -1, mother)
-    rp = ops.xwt_morlet(x1, x2, sj_p, d.delta_t, mother.f0, want_uv=True)
-    u = transforms._np(rp["u"][0], np.float64)
-    v = transforms._np(rp["v"][0], np.float64)
-    return ResultsFromXWT(power, period, sig95, coi_plot, u, v)
+    return run_xwt_batch([cross_wavelet_transform], normalize=normalize)[0]
+
+
+def run_xwt_batch(xwt_data_list: List[DataForXWT], normalize: bool = True
+                  ) -> List[ResultsFromXWT]:
+    """``run_xwt`` over many pairs (engine extension; the reference loops in
+    src/utils/transform_helpers.py:126-135).  Pairs of one length and transform
+    parameters share one normalisation, one pair-mode XWT launch (per-pair AR(1)
+    significance as a [B, S] multiplier) and one phase launch."""
+    out: List[ResultsFromXWT] = [None] * len(xwt_data_list)
+    groups: dict = {}
+    for i, d in enumerate(xwt_data_list):
+        mother = as_morlet(d.mother_wavelet)
+        n1, n2 = np.asarray(d.y1_values).size, np.asarray(d.y2_values).size
+        if n1 != n2:
+            raise ValueError("y1_values and y2_values must have the same length")
+        key = (n1, mother.f0, float(d.delta_t), float(d.delta_j), float(d.initial_scale),
+               tuple(d.levels))
+        groups.setdefault(key, []).append(i)
+    for (n0, f0, dt, dj, s0, levels), idx in groups.items():
+        mother = as_morlet(xwt_data_list[idx[0]].mother_wavelet)
+        d1 = transforms._to_dev(np.stack([np.asarray(xwt_data_list[i].y1_values, dtype=np.float64)
+                                          for i in idx]))
+        d2 = transforms._to_dev(np.stack([np.asarray(xwt_data_list[i].y2_values, dtype=np.float64)
+                                          for i in idx]))
+        m1, m2 = ops.series_moments(d1), ops.series_moments(d2)
+        # pycwt.xwt(normalize=True): (y - mean) / std, in fp64 on the GPU
+        x1 = ops.affine(d1, transforms.normalize_coefs(m1), torch.float32)
+        x2 = ops.affine(d2, transforms.normalize_coefs(m2), torch.float32)
+        sj, freqs = transforms.scales_for(n0, dt, dj, s0, -1, mother)
+        mh1, mh2 = transforms._np(m1), transforms._np(m2)
+        dof = mother.dofmin
+        chi = transforms._chi2_ppf(0.95, dof) / dof
+        signif = []
+        for k in range(len(idx)):
+            g1, _, _ = transforms._ar1_from_moments(mh1[k, 4], mh1[k, 5], int(mh1[k, 6]))
+            g2, _, _ = transforms._ar1_from_moments(mh2[k, 4], mh2[k, 5], int(mh2[k, 6]))
+            Pk1 = transforms.ar1_spectrum(freqs * dt, g1)
+            Pk2 = transforms.ar1_spectrum(freqs * dt, g2)
+            signif.append((Pk1 * Pk2) ** 0.5 * chi)  # std1 = std2 = 1 (normalised, DESIGN 4)
+        signif = np.stack(signif)
+        period = 1 / freqs
+        coi = transforms.cone_of_influence(n0, dt, mother)
+        if normalize:
+            r = ops.xwt_morlet(x1, x2, sj, dt, mother.f0, sig_scale=1.0 / signif,
+                               want_power=True, want_sig=True)
+            power = transforms._np(r["power"], np.float64)
+            sig95 = transforms._np(r["sig"], np.float64)
+            coi_plot = coi_polygon(coi, period, np.log2(levels[2]))
+        else:
+            r = ops.xwt_morlet(x1, x2, sj, dt, mother.f0, want_w12=True)
+            power = transforms._np(r["w12"], np.complex128)
+            sig95 = power / (np.ones([1, n0]) * signif[:, :, None])
+            coi_plot = coi
+        # phase: pycwt.wct(..., delta_j=...) runs at its default dj = 1/12 (quirk B.5)
+        sj_p, _ = transforms.scales_for(n0, dt, 1 / 12, s0, -1, mother)
+        rp = ops.xwt_morlet(x1, x2, sj_p, dt, mother.f0, want_uv=True)
+        u = transforms._np(rp["u"], np.float64)
+        v = transforms._np(rp["v"], np.float64)
+        for k, i in enumerate(idx):
+            out[i] = ResultsFromXWT(power[k], period.copy(), sig95[k], coi_plot.copy(), u[k], v[k])
+    return out
 
 
 def calculate_phase_difference(xwt_phase: npt.NDArray) -> Tuple[npt.NDArray, npt.NDArray]:

@@ -24,8 +24,9 @@ _U64 = C.c_ulonglong
 
 # name -> (restype, argtypes); mirrors include/wtmi.h exactly
 PROTOTYPES = {
-    "wtmi_cwt_morlet": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _F64, _F64, _P, _P, _P, _P, _P]),
-    "wtmi_xwt_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _P,
+    "wtmi_cwt_morlet": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _F64, _F64, _P, _I64, _P, _P,
+                               _P, _P]),
+    "wtmi_xwt_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _P, _I64,
                                _P, _P, _P, _P, _P, _P]),
     "wtmi_wct_workspace_bytes": (_I64, [_I64, _I64, _I32]),
     "wtmi_wct_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _I32,

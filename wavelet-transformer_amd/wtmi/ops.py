@@ -80,6 +80,9 @@ def _f64_dev(a, dev) -> Optional[torch.Tensor]:
             if len(_F64_CACHE) >= _F64_CACHE_MAX:
                 _F64_CACHE.pop(next(iter(_F64_CACHE)))
             _F64_CACHE[key] = t
+    # the cached block may be read by kernels on several streams: tell the caching
+    # allocator about this one, so an eviction cannot recycle it under a running kernel
+    t.record_stream(torch.cuda.current_stream(dev))
     return t
 
 
@@ -113,6 +116,50 @@ def affine(x: torch.Tensor, coef: torch.Tensor, dtype=torch.float32) -> torch.Te
 
 
 # ---------------------------------------------------------------------------- CWT
+# Operand checks run BEFORE anything touches a device: a wrong-sized buffer must never
+# reach a kernel that indexes it by batch and scale (the kernels trust their geometry).
+def _shape(a):
+    return tuple(a.shape) if isinstance(a, torch.Tensor) else np.shape(a)
+
+
+def _n_scales(scales) -> int:
+    shp = _shape(scales)
+    if scales is None or len(shp) != 1 or shp[0] < 1:
+        raise ValueError(f"scales must be a non-empty 1-D array, got shape {shp}")
+    return shp[0]
+
+
+def _check_affine(a, B, name):
+    if a is not None and (not isinstance(a, torch.Tensor) or tuple(a.shape) != (B, 3)):
+        raise ValueError(f"{name} must be a [{B}, 3] tensor, got "
+                         f"{tuple(a.shape) if isinstance(a, torch.Tensor) else type(a).__name__}")
+
+
+def _check_sig(sig_scale, B, S, want_sig):
+    """sig_scale: [S] (every series) or [B, S] (per series); returns sig_ld."""
+    if not want_sig:
+        return 0
+    if sig_scale is None:
+        raise ValueError("want_sig needs sig_scale")
+    shp = _shape(sig_scale)
+    if shp == (S,):
+        return 0
+    if shp == (B, S):
+        return S
+    raise ValueError(f"sig_scale must have shape [{S}] or [{B}, {S}], got {shp}")
+
+
+def _check_out(out, shape, dtype, name):
+    if out is not None and (not isinstance(out, torch.Tensor) or tuple(out.shape) != tuple(shape)
+                            or out.dtype != dtype or not out.is_contiguous()):
+        raise ValueError(f"{name} must be a contiguous {dtype} tensor of shape {tuple(shape)}, got "
+                         f"{_shape(out)} {getattr(out, 'dtype', type(out).__name__)}")
+
+
+def _f64_arg(a, dev):
+    return None if a is None else a.to(device=dev, dtype=torch.float64).contiguous()
+
+
 def cwt_morlet(x: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
                affine: Optional[torch.Tensor] = None, sig_scale=None,
                want_w: bool = True, want_power: bool = False, want_sig: bool = False,
@@ -120,50 +167,68 @@ def cwt_morlet(x: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
     """Morlet CWT of every row of x (float32 [B, n0]) at the given scales.
 
     Returns a dict with any of ``w`` (complex64 [B, S, n0]), ``power`` and ``sig``
-    (float32 [B, S, n0], sig = power * sig_scale[j]).
+    (float32 [B, S, n0], sig = power * sig_scale[j], or sig_scale[b, j] for a [B, S]
+    sig_scale).  Every caller-supplied operand is checked against the launch geometry
+    (shape, dtype, device, contiguity) before the kernel sees it.
     """
     x = _rows(x)
-    dev = _check_dev(x, affine)
+    B, n0 = x.shape
+    S = _n_scales(scales)
+    sig_ld = _check_sig(sig_scale, B, S, want_sig)
+    _check_affine(affine, B, "affine")
+    _check_out(out_w, (B, S, n0), torch.complex64, "out_w")
+    if out_w is not None and not want_w:
+        raise ValueError("out_w given with want_w=False")
+    if not (want_w or want_power or want_sig):
+        raise ValueError("cwt_morlet: no output requested")
+    dev = _check_dev(x, affine, out_w)
     if x.dtype != torch.float32:
         x = x.to(torch.float32)
-    B, n0 = x.shape
     sc = _f64_dev(scales, dev)
-    S = sc.numel()
     ss = _f64_dev(sig_scale, dev) if want_sig else None
-    if want_sig and ss is None:
-        raise ValueError("want_sig needs sig_scale")
+    aff = _f64_arg(affine, dev)
     res = {}
     if want_w:
-        if out_w is None:
-            out_w = torch.empty((B, S, n0), dtype=torch.complex64, device=dev)
-        res["w"] = out_w
+        res["w"] = out_w if out_w is not None else torch.empty((B, S, n0), dtype=torch.complex64,
+                                                               device=dev)
     if want_power:
         res["power"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
     if want_sig:
         res["sig"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
-    aff = affine.to(torch.float64).contiguous() if affine is not None else None
     with torch.cuda.device(dev):
         _lib.call("wtmi_cwt_morlet", _ptr(x), x.stride(0), B, n0, _ptr(aff), _ptr(sc), S,
-                  float(dt), float(f0), _ptr(ss), _ptr(res.get("w")), _ptr(res.get("power")),
-                  _ptr(res.get("sig")), _stream(dev))
+                  float(dt), float(f0), _ptr(ss), sig_ld, _ptr(res.get("w")),
+                  _ptr(res.get("power")), _ptr(res.get("sig")), _stream(dev))
     return res
 
 
-def xwt_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
-               affine1=None, affine2=None, sig_scale=None, want_w12=False, want_power=False,
-               want_sig=False, want_uv=False):
-    """Cross-wavelet outputs of row pairs: any of w12 (complex64), power, sig, u, v."""
+def _pair_rows(x1, x2):
     x1 = _rows(x1).to(torch.float32)
     x2 = _rows(x2).to(torch.float32)
     if x1.shape != x2.shape:
         raise ValueError("x1 and x2 must have the same shape")
     if x1.stride(0) != x2.stride(0):
         x1, x2 = x1.contiguous(), x2.contiguous()
-    dev = _check_dev(x1, x2, affine1, affine2)
+    return x1, x2
+
+
+def xwt_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
+               affine1=None, affine2=None, sig_scale=None, want_w12=False, want_power=False,
+               want_sig=False, want_uv=False):
+    """Cross-wavelet outputs of row pairs: any of w12 (complex64), power, sig, u, v.
+    sig_scale: [S] or per-pair [B, S] (1 / signif)."""
+    x1, x2 = _pair_rows(x1, x2)
     B, n0 = x1.shape
+    S = _n_scales(scales)
+    sig_ld = _check_sig(sig_scale, B, S, want_sig)
+    _check_affine(affine1, B, "affine1")
+    _check_affine(affine2, B, "affine2")
+    if not (want_w12 or want_power or want_sig or want_uv):
+        raise ValueError("xwt_morlet: no output requested")
+    dev = _check_dev(x1, x2, affine1, affine2)
     sc = _f64_dev(scales, dev)
-    S = sc.numel()
     ss = _f64_dev(sig_scale, dev) if want_sig else None
+    a1, a2 = _f64_arg(affine1, dev), _f64_arg(affine2, dev)
     shape = (B, S, n0)
     res = {}
     if want_w12:
@@ -175,11 +240,9 @@ def xwt_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     if want_uv:
         res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
         res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
-    a1 = affine1.to(torch.float64).contiguous() if affine1 is not None else None
-    a2 = affine2.to(torch.float64).contiguous() if affine2 is not None else None
     with torch.cuda.device(dev):
         _lib.call("wtmi_xwt_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
-                  _ptr(sc), S, float(dt), float(f0), _ptr(ss), _ptr(res.get("w12")),
+                  _ptr(sc), S, float(dt), float(f0), _ptr(ss), sig_ld, _ptr(res.get("w12")),
                   _ptr(res.get("power")), _ptr(res.get("sig")), _ptr(res.get("u")),
                   _ptr(res.get("v")), _stream(dev))
     return res
@@ -195,18 +258,19 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
                workspace: Optional[torch.Tensor] = None):
     """Wavelet coherence of row pairs; returns dict coh [B,S,n0] (+ u, v, power =
     |W1 W2*|^2, phase = angle(W1 W2*))."""
-    x1 = _rows(x1).to(torch.float32)
-    x2 = _rows(x2).to(torch.float32)
-    if x1.shape != x2.shape:
-        raise ValueError("x1 and x2 must have the same shape")
-    if x1.stride(0) != x2.stride(0):
-        x1, x2 = x1.contiguous(), x2.contiguous()
-    dev = _check_dev(x1, x2, affine1, affine2)
+    x1, x2 = _pair_rows(x1, x2)
     B, n0 = x1.shape
-    sc = _f64_dev(scales, dev)
-    S = sc.numel()
+    S = _n_scales(scales)
+    _check_affine(affine1, B, "affine1")
+    _check_affine(affine2, B, "affine2")
     need = wct_workspace_bytes(B, n0, S)
-    if workspace is None or workspace.numel() < need:
+    if workspace is not None and (not isinstance(workspace, torch.Tensor) or
+                                  workspace.dtype != torch.uint8 or not workspace.is_contiguous()
+                                  or workspace.numel() < need):
+        raise ValueError(f"workspace must be a contiguous uint8 tensor of >= {need} bytes")
+    dev = _check_dev(x1, x2, affine1, affine2, workspace)
+    sc = _f64_dev(scales, dev)
+    if workspace is None:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     shape = (B, S, n0)
     res = {"coh": torch.empty(shape, dtype=torch.float32, device=dev)}
@@ -217,8 +281,7 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     if want_uv:
         res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
         res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
-    a1 = affine1.to(torch.float64).contiguous() if affine1 is not None else None
-    a2 = affine2.to(torch.float64).contiguous() if affine2 is not None else None
+    a1, a2 = _f64_arg(affine1, dev), _f64_arg(affine2, dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_wct_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
                   _ptr(sc), S, float(dt), float(f0), int(boxcar), _ptr(workspace),
@@ -404,6 +467,63 @@ def _register():
     @_imodwt.register_fake
     def _(w, dec_lo, dec_hi):
         return w.new_empty((w.shape[0] if w.dim() == 3 else 1, w.shape[-1]), dtype=torch.float32)
+
+    def _bs(x, scales, dtype):
+        return x.new_empty((x.shape[0] if x.dim() == 2 else 1, scales.numel(), x.shape[-1]),
+                           dtype=dtype)
+
+    @lib.custom_op("wtmi::xwt", mutates_args=())
+    def _xwt(x1: torch.Tensor, x2: torch.Tensor, scales: torch.Tensor, dt: float, f0: float
+             ) -> torch.Tensor:
+        """W1 W2* (complex64) of row pairs (pycwt.xwt before normalisation)."""
+        return xwt_morlet(x1, x2, scales, dt, f0, want_w12=True)["w12"]
+
+    @_xwt.register_fake
+    def _(x1, x2, scales, dt, f0):
+        return _bs(x1, scales, torch.complex64)
+
+    @lib.custom_op("wtmi::xwt_power", mutates_args=())
+    def _xwt_power(x1: torch.Tensor, x2: torch.Tensor, scales: torch.Tensor, dt: float, f0: float
+                   ) -> torch.Tensor:
+        return xwt_morlet(x1, x2, scales, dt, f0, want_power=True)["power"]
+
+    @_xwt_power.register_fake
+    def _(x1, x2, scales, dt, f0):
+        return _bs(x1, scales, torch.float32)
+
+    @lib.custom_op("wtmi::dwt", mutates_args=())
+    def _dwt(x: torch.Tensor, dec_lo: torch.Tensor, dec_hi: torch.Tensor, level: int
+             ) -> torch.Tensor:
+        """pywt.wavedec (mode symmetric), coefficient lists back-to-back: [B, total]."""
+        return wavedec(x, dec_lo.cpu().numpy(), dec_hi.cpu().numpy(), level)[0]
+
+    @_dwt.register_fake
+    def _(x, dec_lo, dec_hi, level):
+        total = sum(dwt_lengths(x.shape[-1], dec_lo.numel(), level))
+        return x.new_empty((x.shape[0] if x.dim() == 2 else 1, total), dtype=torch.float32)
+
+    @lib.custom_op("wtmi::idwt", mutates_args=())
+    def _idwt(coeffs: torch.Tensor, n: int, rec_lo: torch.Tensor, rec_hi: torch.Tensor,
+              level: int) -> torch.Tensor:
+        """pywt.waverec of back-to-back coefficient lists: [B, out_len]."""
+        full = (1 << (level + 1)) - 1
+        return waverec(coeffs, n, rec_lo.cpu().numpy(), rec_hi.cpu().numpy(), level, [full])[:, 0]
+
+    @_idwt.register_fake
+    def _(coeffs, n, rec_lo, rec_hi, level):
+        lens = dwt_lengths(n, rec_lo.numel(), level)
+        out_len = 2 * lens[-1] - rec_lo.numel() + 2 if level > 0 else n
+        return coeffs.new_empty((coeffs.shape[0] if coeffs.dim() == 2 else 1, out_len),
+                                dtype=torch.float32)
+
+    @lib.custom_op("wtmi::series_stats", mutates_args=())
+    def _series_stats(x: torch.Tensor) -> torch.Tensor:
+        """[B, 8] float64: mean, std, detrend slope, intercept, lag-0 / lag-1 covariance, n, 0."""
+        return series_moments(x)
+
+    @_series_stats.register_fake
+    def _(x):
+        return x.new_empty((x.shape[0] if x.dim() == 2 else 1, 8), dtype=torch.float64)
 
 
 try:

@@ -1,12 +1,15 @@
-"""Put the engine's six drop-in modules into an unchanged reference checkout.
+"""Put the engine's seven drop-in modules into an unchanged reference checkout.
 
 The reference app imports ``from src import cwt, dwt, wct, xwt`` and
 ``src.utils.wavelet_helpers`` (src/wavelet_plots.py:15-26, src/utils/transform_helpers.py:8-13,
-src/utils/plot_helpers.py:8-10, src/regression.py:16-19).  Everything else under the
-reference's ``src`` (retrieve_data, helpers, file_helpers, wavelet_plots, ...) must keep
-resolving to the reference's own files.  So exactly these module names are replaced:
+src/utils/plot_helpers.py:8-10, src/regression.py:16-19), and builds its per-series
+results through ``src.utils.transform_helpers`` (src/wavelet_plots.py:25, src/regression.py:16).
+Everything else under the reference's ``src`` (retrieve_data, helpers, file_helpers,
+wavelet_plots, ...) must keep resolving to the reference's own files.  So exactly these
+module names are replaced:
 
     src.cwt  src.xwt  src.wct  src.dwt  src.modwt  src.utils.wavelet_helpers
+    src.utils.transform_helpers   (the batch API: one launch per group of series)
 
 The repository's own ``src`` directory has no ``__init__.py`` (a namespace package): a
 reference checkout's regular ``src`` package always wins over it, whatever the order on
@@ -16,15 +19,15 @@ Two ways to activate it, neither edits the app's code:
 
 1. Import hook (nothing written into the reference tree)::
 
-       python -m wtmi.overlay run -- streamlit run app.py      # from the reference root
+       python -m wtmi.overlay run streamlit run app.py      # from the reference root
 
-   installs a ``sys.meta_path`` finder that serves the six names from this repository and
+   installs a ``sys.meta_path`` finder that serves the seven names from this repository and
    then runs the given module (``streamlit``) in the same process.  In-process users call
    ``wtmi.overlay.install()`` before the first ``import src.cwt``.
 
 2. Stub files (for deployments that start the app themselves)::
 
-       python -m wtmi.overlay stubs /path/to/reference      # writes 6 stubs, keeps *.orig
+       python -m wtmi.overlay stubs /path/to/reference      # writes 7 stubs, keeps *.orig
        python -m wtmi.overlay restore /path/to/reference    # puts the originals back
 
    Each stub is a three-line module that executes this repository's module of the same
@@ -48,6 +51,7 @@ MODULES = {
     "src.dwt": "src/dwt.py",
     "src.modwt": "src/modwt.py",
     "src.utils.wavelet_helpers": "src/utils/wavelet_helpers.py",
+    "src.utils.transform_helpers": "src/utils/transform_helpers.py",
 }
 STUB_MARK = "# wtmi overlay stub"
 
@@ -64,7 +68,7 @@ def _ensure_engine_importable():
 
 
 class OverlayFinder(importlib.abc.MetaPathFinder):
-    """Serves the six replaced module names from this repository; declines all others."""
+    """Serves the replaced module names from this repository; declines all others."""
 
     def find_spec(self, fullname, path=None, target=None):
         if fullname not in MODULES:
@@ -76,8 +80,8 @@ _FINDER = OverlayFinder()
 
 
 def install() -> None:
-    """Activate the import hook (idempotent).  Modules already imported under the six
-    names are dropped so that the next import resolves through the hook."""
+    """Activate the import hook (idempotent).  Modules already imported under the
+    replaced names are dropped so that the next import resolves through the hook."""
     _ensure_engine_importable()
     if _FINDER not in sys.meta_path:
         sys.meta_path.insert(0, _FINDER)
@@ -109,7 +113,7 @@ def _stub_text(name: str) -> str:
 
 
 def write_stubs(reference_root: str) -> list[str]:
-    """Replace the six reference files by stubs; each original is kept as ``<file>.orig``."""
+    """Replace the reference files by stubs; each original is kept as ``<file>.orig``."""
     written = []
     for name in MODULES:
         rel = name.replace(".", "/") + ".py"
@@ -142,7 +146,7 @@ def main(argv=None) -> int:
     r = sub.add_parser("run", help="install the import hook, then run a module (e.g. streamlit)")
     r.add_argument("module")
     r.add_argument("args", nargs=argparse.REMAINDER)
-    s = sub.add_parser("stubs", help="write the six stub modules into a reference checkout")
+    s = sub.add_parser("stubs", help="write the stub modules into a reference checkout")
     s.add_argument("reference_root")
     u = sub.add_parser("restore", help="put the reference's original modules back")
     u.add_argument("reference_root")
@@ -158,7 +162,7 @@ def main(argv=None) -> int:
     if os.getcwd() not in sys.path:
         sys.path.insert(0, os.getcwd())  # the app's root, as `python -m` would give it
     install()
-    args = [x for x in a.args if x != "--"] if a.args[:1] == ["--"] else a.args
+    args = a.args[1:] if a.args[:1] == ["--"] else a.args
     sys.argv = [a.module] + args
     runpy.run_module(a.module, run_name="__main__", alter_sys=True)
     return 0

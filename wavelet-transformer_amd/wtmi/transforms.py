@@ -335,6 +335,58 @@ def significance_from_histogram(wlc: np.ndarray, anyout: np.ndarray, maxscale: i
 
 
 _sig_cache: dict = {}
+_sig_cache_lock = threading.Lock()
+
+
+def sig_cache_dir() -> str:
+    """Directory of the persistent significance cache: $WTMI_CACHE_DIR, else
+    ~/.cache/wtmi/wct_sig (pycwt keeps its own under the user cache dir)."""
+    import os
+    root = os.environ.get("WTMI_CACHE_DIR") or os.path.join(os.path.expanduser("~"), ".cache", "wtmi")
+    return os.path.join(root, "wct_sig")
+
+
+def _sig_cache_path(key) -> str:
+    import hashlib
+    import os
+    h = hashlib.sha256(repr(key).encode()).hexdigest()[:32]
+    return os.path.join(sig_cache_dir(), f"sig95_{h}.npy")
+
+
+def sig_cache_load(key):
+    """sig95 for a wct_significance argument key: process memory first, then disk."""
+    import os
+    with _sig_cache_lock:
+        if key in _sig_cache:
+            return _sig_cache[key].copy()
+    path = _sig_cache_path(key)
+    if os.path.exists(path):
+        try:
+            arr = np.load(path, allow_pickle=False)
+        except (OSError, ValueError):
+            return None  # unreadable entry: recompute (and overwrite it)
+        with _sig_cache_lock:
+            _sig_cache[key] = arr.copy()
+        return arr
+    return None
+
+
+def sig_cache_store(key, sig95) -> None:
+    """Keep sig95 in memory and on disk (atomic rename; a failed write only costs a
+    recomputation later)."""
+    import os
+    import tempfile
+    with _sig_cache_lock:
+        _sig_cache[key] = np.array(sig95, copy=True)
+    d = sig_cache_dir()
+    try:
+        os.makedirs(d, exist_ok=True)
+        fd, tmp = tempfile.mkstemp(dir=d, suffix=".npy")
+        with os.fdopen(fd, "wb") as fh:
+            np.save(fh, np.asarray(sig95, dtype=np.float64), allow_pickle=False)
+        os.replace(tmp, _sig_cache_path(key))
+    except OSError:
+        pass
 
 
 def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="morlet",
@@ -343,13 +395,16 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     """pycwt ``wct_significance`` on the GPU: mc_count passes of two AR(1) red-noise
     series (al1, al2), their coherence, and the per-scale counter of floor(R2 * nbins)
     outside the COI, batched max_pairs_per_launch passes per launch.  ``cache`` keeps
-    results in process memory keyed on every argument (pycwt keeps a disk cache);
+    results keyed on every argument, in process memory and on disk (``sig_cache_dir()``),
+    as pycwt's ``cache=True`` keeps them under the user cache dir (src/wct.py:117);
     ``seed`` None draws a fresh one, as pycwt's unseeded draws do."""
     wavelet = as_morlet(wavelet)
-    key = (float(al1), float(al2), float(dt), float(dj), float(s0), int(J),
-           float(significance_level), wavelet.f0, int(mc_count), nbins, seed)
-    if cache and key in _sig_cache:
-        return _sig_cache[key].copy()
+    key = ("wct_significance", 1, float(al1), float(al2), float(dt), float(dj), float(s0), int(J),
+           float(significance_level), wavelet.f0, int(mc_count), int(nbins), seed)
+    if cache:
+        hit = sig_cache_load(key)
+        if hit is not None:
+            return hit
     N, sj, t_lo, t_hi, anyout, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
     if seed is None:
         seed = int(np.random.SeedSequence().entropy) & ((1 << 64) - 1)
@@ -374,7 +429,7 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     full[:wlc.shape[0]] = wlc[:maxscale] if maxscale > 0 else 0
     sig95 = significance_from_histogram(full, anyout, maxscale, significance_level)
     if cache:
-        _sig_cache[key] = sig95.copy()
+        sig_cache_store(key, sig95)
     return sig95
 
 
@@ -412,6 +467,22 @@ def wavedec(data, wavelet, mode="symmetric", level=None):
         out.append(flat[off:off + L])
         off += L
     return out
+
+
+def wavedec_batch(rows, wavelet, level=None):
+    """wavedec of several series of one length in ONE launch: list of coefficient lists."""
+    w = as_filter_bank(wavelet)
+    x = np.asarray(rows)
+    if x.ndim != 2:
+        raise ValueError("wavedec_batch expects [batch, n]")
+    if level is None:
+        level = dwt_max_level(x.shape[1], w.dec_len)
+    if level < 0:
+        raise ValueError(f"Level value of {level} is too low . Minimum level is 0.")
+    coeffs, lens = ops.wavedec(_to_dev(x, torch.float32), w.dec_lo, w.dec_hi, level)
+    flat = _np(coeffs, np.float64)
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    return [[flat[b, offs[k]:offs[k + 1]] for k in range(len(lens))] for b in range(x.shape[0])]
 
 
 def _pack_coeffs(coeffs, dec_len):
