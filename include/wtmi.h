@@ -29,7 +29,8 @@ extern "C" {
 /* ---- CWT (K1+K2) --------------------------------------------------------------
  * Replaces pycwt.cwt(signal, dt, dj, s0, J, Morlet(f0)) as called from
  * src/cwt.py:110-112 (power |W|^2 at :114, significance ratio at :123-133).
- * x: [batch][ld] float32, n0 <= 16384 samples used per series.
+ * x: [batch][ld] float32, n0 <= 2^20 samples used per series (above 16384 the long-row
+ *    path runs: see wtmi_cwt_workspace_bytes).
  * affine: optional [batch][3] float64 (a0, a1, a2): x' = (x - a0 - a1*t) * a2 applied
  *         before the transform (standardize_series / pycwt normalisation), or NULL.
  * scales: [n_scales] float64 (s_j).  sig_scale: float64 1/signif_j, series b reading
@@ -41,7 +42,13 @@ extern "C" {
 int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
                     const double* affine, const double* scales, int n_scales, double dt,
                     double f0, const double* sig_scale, long long sig_ld, float* out_w,
-                    float* out_power, float* out_sig, void* stream);
+                    float* out_power, float* out_sig, void* workspace, void* stream);
+
+/* Device scratch a CWT (pair = 0) or XWT (pair = 1) call needs: 0 for n0 <= 16384 (one
+ * workgroup holds a row; workspace may be NULL), else the four-step long-row path's
+ * spectra and work rows (bounded: series and scales are processed in chunks of about
+ * 1 GiB each).  Rows up to 2^20 samples; longer ones return kErrUnsupported.         */
+long long wtmi_cwt_workspace_bytes(long long batch, long long n0, int n_scales, int pair);
 
 /* ---- XWT / phase (K1+K2, pair mode) ------------------------------------------
  * Replaces the two pycwt.cwt calls and W1*conj(W2) inside pycwt.xwt
@@ -53,7 +60,7 @@ int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long ba
                     long long n0, const double* affine1, const double* affine2,
                     const double* scales, int n_scales, double dt, double f0,
                     const double* sig_scale, long long sig_ld, float* out_w12, float* out_power,
-                    float* out_sig, float* out_u, float* out_v, void* stream);
+                    float* out_sig, float* out_u, float* out_v, void* workspace, void* stream);
 
 /* ---- WCT coherence + XWT power / phase (K1+K2+K7+K8) ---------------------------
  * Replaces pycwt.wct(..., sig=False) numerics (src/wct.py:106-118): two CWTs,
@@ -92,12 +99,16 @@ int wtmi_coherence_histogram(const float* coh, long long batch, long long n0, in
  * dec_lo/dec_hi: HOST pointers to the n_taps analysis filters (pywt dec_lo/dec_hi);
  * the kernels use h~ = dec_hi/sqrt2, g~ = dec_lo/sqrt2 (n_taps <= 128).
  * w: [batch][level+1][n] float32.  keep_mask (imodwt): bit r set = row r used, others
- * treated as zero (modwtmra / smooth_signal, src/modwt.py:163-251); ~0ull = all.    */
+ * treated as zero (modwtmra / smooth_signal, src/modwt.py:163-251); ~0ull = all.
+ * workspace: NULL for n <= 16384 (a series lives in one workgroup's LDS); longer series
+ * run one launch per level and need wtmi_modwt_workspace_bytes() of device scratch.  */
+long long wtmi_modwt_workspace_bytes(long long batch, long long n, int level);
 int wtmi_modwt(const float* x, long long ld, long long batch, long long n, const double* dec_lo,
-               const double* dec_hi, int n_taps, int level, float* w, void* stream);
+               const double* dec_hi, int n_taps, int level, float* w, void* workspace,
+               void* stream);
 int wtmi_imodwt(const float* w, long long batch, long long n, const double* dec_lo,
                 const double* dec_hi, int n_taps, int level, unsigned long long keep_mask,
-                float* x, long long ld_out, void* stream);
+                float* x, long long ld_out, void* workspace, void* stream);
 
 /* ---- DWT (K5 / K6) -------------------------------------------------------------
  * Replace pywt.wavedec / pywt.waverec with mode "symmetric" (src/dwt.py:104,120;
@@ -106,14 +117,18 @@ int wtmi_imodwt(const float* w, long long batch, long long n, const double* dec_
  * the per-array lengths (host, lens[level+1]) and returns the total per series.
  * waverec: n_variants reconstructions per series, variant v keeps array k when bit k
  * of keep_masks[v] is set (ResultsFromDWT.smooth_signal, reconstruct_signal_component,
- * src/dwt.py:53-73,110-120); out: [batch][n_variants][out_len].                   */
+ * src/dwt.py:53-73,110-120); out: [batch][n_variants][out_len].
+ * workspace: NULL for n <= 16384; longer series run one launch per level and need
+ * wtmi_dwt_workspace_bytes(batch, n, n_taps, n_variants) (wavedec: n_variants = 1).  */
 long long wtmi_dwt_lengths(long long n, int n_taps, int level, long long* lens);
+long long wtmi_dwt_workspace_bytes(long long batch, long long n, int n_taps, int n_variants);
 int wtmi_wavedec(const float* x, long long ld, long long batch, long long n, const double* dec_lo,
-                 const double* dec_hi, int n_taps, int level, float* coeffs, void* stream);
+                 const double* dec_hi, int n_taps, int level, float* coeffs, void* workspace,
+                 void* stream);
 int wtmi_waverec(const float* coeffs, long long batch, long long n, const double* rec_lo,
                  const double* rec_hi, int n_taps, int level,
                  const unsigned long long* keep_masks, int n_variants, float* out,
-                 long long out_len, void* stream);
+                 long long out_len, void* workspace, void* stream);
 
 /* ---- per-series moments / affine (K9) -----------------------------------------
  * Replace standardize_series (src/utils/wavelet_helpers.py:22-57) and the

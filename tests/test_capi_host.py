@@ -42,9 +42,13 @@ def test_invalid_arguments_rejected_without_gpu():
     from wtmi import _lib
     lib = _lib.load()
     assert lib.wtmi_cwt_morlet(None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, 0, None, None,
-                               None, None) == -1
-    assert lib.wtmi_modwt(None, 16, 1, 16, None, None, 8, 2, None, None) == -1
-    assert lib.wtmi_wavedec(None, 16, 1, 16, None, None, 8, 2, None, None) == -1
+                               None, None, None) == -1
+    assert lib.wtmi_cwt_workspace_bytes(4, 16384, 10, 0) == 0
+    assert lib.wtmi_cwt_workspace_bytes(4, 16385, 10, 1) > 2 * 4 * 32768 * 8
+    assert lib.wtmi_modwt(None, 16, 1, 16, None, None, 8, 2, None, None, None) == -1
+    assert lib.wtmi_wavedec(None, 16, 1, 16, None, None, 8, 2, None, None, None) == -1
+    assert lib.wtmi_modwt_workspace_bytes(3, 16384, 10) == 0 and lib.wtmi_modwt_workspace_bytes(3, 20000, 10) == 3 * 20000 * 4
+    assert lib.wtmi_dwt_workspace_bytes(2, 16384, 8, 1) == 0 and lib.wtmi_dwt_workspace_bytes(2, 20000, 8, 3) > 0
     assert lib.wtmi_series_moments(None, 0, 1, 1, 1, None, None) == -1
     with pytest.raises(_lib.WtmiError, match="invalid argument"):
         _lib.call("wtmi_affine", None, 0, 1, 1, 1, None, None, 0, 1, None)

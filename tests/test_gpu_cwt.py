@@ -140,7 +140,7 @@ def test_rejects_cpu_tensors_and_bad_args():
     from wtmi import _lib
     with pytest.raises(_lib.WtmiError):
         _lib.call("wtmi_cwt_morlet", None, 0, 1, 16, None, None, 1, 1.0, 6.0, None, 0, None, None,
-                  None, None)
+                  None, None, None)
 
 
 def test_torch_custom_ops_match_oracle(db4):
@@ -191,7 +191,7 @@ def test_torch_custom_ops_xwt_dwt_stats(db4):
     st = torch.ops.wtmi.series_stats(d1).cpu().numpy()
     np.testing.assert_allclose(st[:, 0], x1.astype(np.float64).mean(axis=1), rtol=1e-9)
     np.testing.assert_allclose(st[:, 1], x1.astype(np.float64).std(axis=1), rtol=1e-9)
-    with FakeTensorMode():
+    with FakeTensorMode(allow_non_fake_inputs=True):
         f1 = torch.empty(2, n0, device="cuda")
         fs = torch.empty(sj.numel(), dtype=torch.float64, device="cuda")
         assert torch.ops.wtmi.xwt(f1, f1, fs, dt, 6.0).shape == W12.shape

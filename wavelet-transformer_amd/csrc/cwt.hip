@@ -11,6 +11,7 @@
 // {W1 W2*, |W1 W2*|^2, ratio, phase arrows u = sin(angle), v = cos(angle)}).
 // The Morlet filter is evaluated in-register: no filter bank is read from HBM.
 #include "cwt_common.hpp"
+#include "long_path.hpp"
 
 namespace wtmi {
 
@@ -353,12 +354,14 @@ using namespace wtmi;
 extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
                                const double* affine, const double* scales, int n_scales,
                                double dt, double f0, const double* sig_scale, long long sig_ld,
-                               float* out_w, float* out_power, float* out_sig, void* stream) {
+                               float* out_w, float* out_power, float* out_sig, void* workspace,
+                               void* stream) {
   if (!x || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
   if (sig_ld != 0 && sig_ld < n_scales) return kErrArg;
   if (!out_w && !out_power && !out_sig) return kErrArg;
   if (out_sig && !sig_scale) return kErrArg;
-  if (n0 > (1 << 14)) return kErrUnsupported;
+  if (n0 > (1ll << kLongMaxLog)) return kErrUnsupported;
+  if (n0 > (1 << 14) && !workspace) return kErrArg;
   CwtArgs a{};
   a.x = x;
   a.ld = ld;
@@ -374,6 +377,7 @@ extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, lo
   a.out_w = reinterpret_cast<cpx*>(out_w);
   a.out_pow = out_power;
   a.out_sig = out_sig;
+  if (n0 > (1 << 14)) return batch && n_scales ? cwt_long(a, false, workspace, static_cast<hipStream_t>(stream)) : kOk;
   return dispatch<0>(a, static_cast<hipStream_t>(stream));
 }
 
@@ -382,13 +386,14 @@ extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, l
                                const double* scales, int n_scales, double dt, double f0,
                                const double* sig_scale, long long sig_ld, float* out_w12,
                                float* out_power, float* out_sig, float* out_u, float* out_v,
-                               void* stream) {
+                               void* workspace, void* stream) {
   if (!x1 || !x2 || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
   if (sig_ld != 0 && sig_ld < n_scales) return kErrArg;
   if (!out_w12 && !out_power && !out_sig && !out_u) return kErrArg;
   if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
   if (out_sig && !sig_scale) return kErrArg;
-  if (n0 > (1 << 14)) return kErrUnsupported;
+  if (n0 > (1ll << kLongMaxLog)) return kErrUnsupported;
+  if (n0 > (1 << 14) && !workspace) return kErrArg;
   CwtArgs a{};
   a.x = x1;
   a.x2 = x2;
@@ -408,5 +413,6 @@ extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, l
   a.out_sig = out_sig;
   a.out_u = out_u;
   a.out_v = out_v;
+  if (n0 > (1 << 14)) return batch && n_scales ? cwt_long(a, true, workspace, static_cast<hipStream_t>(stream)) : kOk;
   return dispatch<1>(a, static_cast<hipStream_t>(stream));
 }

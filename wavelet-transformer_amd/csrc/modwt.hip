@@ -17,7 +17,8 @@
 namespace wtmi {
 
 constexpr int kMaxTaps = 128;
-constexpr int kModwtMaxN = 16384;
+constexpr int kModwtMaxN = 16384;          // one workgroup, series in LDS
+constexpr long long kModwtLongMaxN = 1ll << 30;  // per-level launches (int sample index)
 constexpr int kModwtMaxPerThread = 16;  // scalars per thread (n <= 16 * block)
 
 struct FilterBank {
@@ -555,6 +556,105 @@ __global__ void __launch_bounds__(T, 1)
   for (int q = tid; q < ng; q += T) xo[q] = V4[vp(q)];
 }
 
+// ---------------------------------------------------------------------------------
+// Long series (n > 16384: V no longer fits one workgroup's LDS).  One launch per level,
+// one thread per (series, sample); the L taps of V_{j-1} come through L1/L2 (they lie
+// within (L-1) 2^(j-1) samples of each other), V ping-pongs between a [batch][n] scratch
+// row and the output's V_J row, arranged so that the last level lands in row J.
+__global__ void __launch_bounds__(256) modwt_level_kernel(const float* __restrict__ vin, long long ld_in,
+                                                          long long batch, int n, int dm, int L,
+                                                          FilterBank fb, float* __restrict__ wout,
+                                                          long long ld_w, float* __restrict__ vout,
+                                                          long long ld_v) {
+  const long long idx = blockIdx.x * 256ll + threadIdx.x;
+  if (idx >= batch * n) return;
+  const long long b = idx / n;
+  const int t = static_cast<int>(idx - b * n);
+  const float* v = vin + b * ld_in;
+  float aw = 0.f, av = 0.f;
+  int p = t;
+  for (int l = 0; l < L; ++l) {  // taps at (t - dm l) mod n, dm < n
+    const float s = v[p];
+    aw = fmaf(fb.h[l], s, aw);
+    av = fmaf(fb.g[l], s, av);
+    p -= dm;
+    if (p < 0) p += n;
+  }
+  wout[b * ld_w + t] = aw;
+  vout[b * ld_v + t] = av;
+}
+
+__global__ void __launch_bounds__(256) imodwt_level_kernel(const float* __restrict__ w, long long ld_w,
+                                                           const float* __restrict__ vin, long long ld_in,
+                                                           long long batch, int n, int dm, int L, float wsel,
+                                                           float vsel, FilterBank fb, float* __restrict__ vout,
+                                                           long long ld_out) {
+  const long long idx = blockIdx.x * 256ll + threadIdx.x;
+  if (idx >= batch * n) return;
+  const long long b = idx / n;
+  const int t = static_cast<int>(idx - b * n);
+  const float* wr = w + b * ld_w;
+  const float* vr = vin + b * ld_in;
+  float acc = 0.f;
+  int p = t;
+  for (int l = 0; l < L; ++l) {  // taps at (t + dm l) mod n
+    acc = fmaf(vsel * fb.g[l], vr[p], acc);
+    acc = fmaf(wsel * fb.h[l], wr[p], acc);
+    p += dm;
+    if (p >= n) p -= n;
+  }
+  vout[b * ld_out + t] = acc;
+}
+
+static int modwt_long(const float* x, long long ld, long long batch, int n, const FilterBank& fb, int L,
+                      int level, float* w, float* scratch, hipStream_t st) {
+  const long long grid = (batch * n + 255) / 256;
+  if (grid > 0x7fffffffll) return kErrUnsupported;
+  const long long ldw = static_cast<long long>(level + 1) * n;
+  const float* vin = x;
+  long long ldin = ld;
+  for (int j = 1; j <= level; ++j) {
+    const int dm = static_cast<int>((1ll << (j - 1)) % n);
+    // V_j into row J when (level - j) is even, else into the [batch][n] scratch
+    const bool to_row = (level - j) % 2 == 0;
+    float* vout = to_row ? w + static_cast<long long>(level) * n : scratch;
+    const long long ldv = to_row ? ldw : static_cast<long long>(n);
+    hipLaunchKernelGGL(modwt_level_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, vin, ldin,
+                       batch, n, dm, L, fb, w + static_cast<long long>(j - 1) * n, ldw, vout, ldv);
+    const int rc = launch_status();
+    if (rc != kOk) return rc;
+    vin = vout;
+    ldin = ldv;
+  }
+  return kOk;
+}
+
+static int imodwt_long(const float* w, long long batch, int n, const FilterBank& fb, int L, int level,
+                       unsigned long long keep, float* x, long long ld_out, float* scratch, hipStream_t st) {
+  const long long grid = (batch * n + 255) / 256;
+  if (grid > 0x7fffffffll) return kErrUnsupported;
+  const long long ldw = static_cast<long long>(level + 1) * n;
+  const float* vin = w + static_cast<long long>(level) * n;
+  long long ldin = ldw;
+  float vsel = ((keep >> level) & 1ull) ? 1.f : 0.f;  // a dropped V_J row counts as zero
+  for (int j = level; j >= 1; --j) {
+    const int dm = static_cast<int>((1ll << (j - 1)) % n);
+    const float wsel = ((keep >> (j - 1)) & 1ull) ? 1.f : 0.f;
+    // V_{j-1} into x when (j - 1) is even, else into scratch: level 1 writes x
+    float* vout = ((j - 1) % 2 == 0) ? x : scratch;
+    const long long ldo = ((j - 1) % 2 == 0) ? ld_out : static_cast<long long>(n);
+    hipLaunchKernelGGL(imodwt_level_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st,
+                       w + static_cast<long long>(j - 1) * n, ldw, vin, ldin, batch, n, dm, L, wsel, vsel,
+                       fb, vout, ldo);
+    const int rc = launch_status();
+    if (rc != kOk) return rc;
+    vin = vout;
+    ldin = ldo;
+    vsel = 1.f;
+  }
+  return kOk;
+}
+
 static int modwt_block(int n) {
   int t = (n + kModwtMaxPerThread - 1) / kModwtMaxPerThread;
   t = ((t + 63) / 64) * 64;
@@ -582,14 +682,26 @@ static void allow_lds(K kernel, size_t bytes) {
 
 using namespace wtmi;
 
+extern "C" long long wtmi_modwt_workspace_bytes(long long batch, long long n, int level) {
+  if (batch < 0 || n < 0 || level < 1) return -1;
+  if (n <= kModwtMaxN) return 0;
+  // one [batch][n] float row: the analysis's and the synthesis's V ping-pong partner
+  return batch * n * static_cast<long long>(sizeof(float));
+}
+
 extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long long n,
                           const double* dec_lo, const double* dec_hi, int n_taps, int level,
-                          float* w, void* stream) {
+                          float* w, void* workspace, void* stream) {
   FilterBank fb;
   if (!x || !w || batch < 0 || n < 1 || ld < n || level < 1 || level > 62) return kErrArg;
   if (!make_bank(dec_lo, dec_hi, n_taps, fb)) return kErrArg;
-  if (n > kModwtMaxN || batch > 0x7fffffffll) return kErrUnsupported;
+  if (n > kModwtLongMaxN || batch > 0x7fffffffll) return kErrUnsupported;
   if (batch == 0) return kOk;
+  if (n > kModwtMaxN) {
+    if (!workspace) return kErrArg;
+    return modwt_long(x, ld, batch, static_cast<int>(n), fb, n_taps, level, w, static_cast<float*>(workspace),
+                      static_cast<hipStream_t>(stream));
+  }
   const int ni = static_cast<int>(n);
   const size_t lds = static_cast<size_t>((ni + 3) & ~3) * sizeof(float);
   const int block = modwt_block(ni);
@@ -624,12 +736,17 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
 
 extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const double* dec_lo,
                            const double* dec_hi, int n_taps, int level, unsigned long long keep_mask,
-                           float* x, long long ld_out, void* stream) {
+                           float* x, long long ld_out, void* workspace, void* stream) {
   FilterBank fb;
   if (!x || !w || batch < 0 || n < 1 || ld_out < n || level < 1 || level > 62) return kErrArg;
   if (!make_bank(dec_lo, dec_hi, n_taps, fb)) return kErrArg;
-  if (n > kModwtMaxN || batch > 0x7fffffffll) return kErrUnsupported;
+  if (n > kModwtLongMaxN || batch > 0x7fffffffll) return kErrUnsupported;
   if (batch == 0) return kOk;
+  if (n > kModwtMaxN) {
+    if (!workspace) return kErrArg;
+    return imodwt_long(w, batch, static_cast<int>(n), fb, n_taps, level, keep_mask, x, ld_out,
+                       static_cast<float*>(workspace), static_cast<hipStream_t>(stream));
+  }
   const int ni = static_cast<int>(n);
   const size_t lds = 2 * static_cast<size_t>((ni + 3) & ~3) * sizeof(float);
   const int block = modwt_block(ni);

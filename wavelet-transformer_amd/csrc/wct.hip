@@ -17,6 +17,7 @@
 // Phase B (one thread = one time column of one pair): streams the S rows of T once,
 // keeps the last K rows in registers and writes WCT.
 #include "cwt_common.hpp"
+#include "long_path.hpp"
 
 namespace wtmi {
 
@@ -813,6 +814,173 @@ static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0,
   return launch_status();
 }
 
+// Phase B for any boxcar width (K > 24, where the register ring of wct_phase_b would not
+// fit): each output row sums its K window rows straight from the workspace (K loads per
+// output instead of one) -- the same weights and the same rows.
+__global__ void __launch_bounds__(256) wct_phase_b_generic(const cpx* __restrict__ TA,
+                                                           const cpx* __restrict__ TB, long long batch,
+                                                           int n0, int S, int K, float* __restrict__ coh,
+                                                           const int* __restrict__ plan) {
+  const long long tiles = (n0 + 255) / 256;
+  const long long b = blockIdx.x / tiles;
+  const int u = static_cast<int>((blockIdx.x - b * tiles) * 256 + threadIdx.x);
+  if (u >= n0) return;
+  const int LO = K / 2;
+  const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
+  const long long base = b * static_cast<long long>(S) * n0 + u;
+  const int last = plan[S];
+  for (int i = 0; i <= last && i < S; ++i) {
+    if (plan[i] & kPlanSpec) continue;
+    float s1 = 0.f, s2 = 0.f, re = 0.f, im = 0.f;
+    for (int q = 0; q < K; ++q) {
+      const int row = i - LO + q;
+      if (row < 0 || row >= S) continue;
+      const float wq = (K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn;
+      const cpx ta = TA[base + static_cast<long long>(row) * n0];
+      const cpx tb = TB[base + static_cast<long long>(row) * n0];
+      s1 = fmaf(wq, ta.x, s1);
+      s2 = fmaf(wq, ta.y, s2);
+      re = fmaf(wq, tb.x, re);
+      im = fmaf(wq, tb.y, im);
+    }
+    coh[base + static_cast<long long>(i) * n0] = fast_div(re * re + im * im, s1 * s2);
+  }
+}
+
+int wct_phase_b_any(const cpx* TA, const cpx* TB, long long batch, int n0, int S, float* coh,
+                    const int* plan, int K, hipStream_t st) {
+  switch (K) {
+#define WTMI_B(KK) case KK: return launch_phase_b<KK>(TA, TB, batch, n0, S, coh, plan, st);
+    WTMI_B(1) WTMI_B(2) WTMI_B(3) WTMI_B(4) WTMI_B(5) WTMI_B(6) WTMI_B(7) WTMI_B(8)
+    WTMI_B(9) WTMI_B(10) WTMI_B(11) WTMI_B(12) WTMI_B(13) WTMI_B(14) WTMI_B(15) WTMI_B(16)
+    WTMI_B(17) WTMI_B(18) WTMI_B(19) WTMI_B(20) WTMI_B(21) WTMI_B(22) WTMI_B(23) WTMI_B(24)
+#undef WTMI_B
+    default: break;
+  }
+  if (K < 1) return kErrArg;
+  const long long grid = batch * ((n0 + 255) / 256);
+  if (grid > 0x7fffffffll) return kErrUnsupported;
+  hipLaunchKernelGGL(wct_phase_b_generic, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB, batch,
+                     n0, S, K, coh, plan);
+  return launch_status();
+}
+
+// Rows of at most 8 samples (N <= 8, below the FFT engine's 16-point minimum): the whole
+// pycwt.wct of one pair in one workgroup by direct DFTs in fp64 -- two CWTs, the time
+// Gaussian of |W1|^2/s, |W2|^2/s, W12/s through length-N DFTs, then the scale boxcar and
+// the ratio (src/wct.py:106-118 at n0 <= 8).  Smoothed rows sit in LDS ([S][n0] x 4 floats).
+constexpr size_t kWctDirectMaxLds = 150 * 1024;  // S * n0 <= 9600 smoothed points
+
+__global__ void __launch_bounds__(256) wct_direct_kernel(CwtArgs a, int N, int K, float* __restrict__ coh) {
+  extern __shared__ float4 tsm[];  // [S][n0]: (T1, T2, Re T12, Im T12)
+  __shared__ double2 X[2][8];
+  const long long b = blockIdx.x;
+  const int n0 = a.n0, S = a.S;
+  if (threadIdx.x < 2 * N) {  // spectra of the two (affine-normalised) series
+    const int which = threadIdx.x / N, k = threadIdx.x % N;
+    const float* row = (which ? a.x2 : a.x) + b * a.ld;
+    const double* af = which ? a.affine2 : a.affine;
+    double re = 0.0, im = 0.0;
+    for (int n = 0; n < n0; ++n) {
+      double v = row[n];
+      if (af) v = static_cast<float>((v - af[3 * b] - af[3 * b + 1] * n) * af[3 * b + 2]);
+      double sn, cs;
+      sincospi(-2.0 * ((k * n) % N) / N, &sn, &cs);
+      re += v * cs;
+      im += v * sn;
+    }
+    X[which][k] = make_double2(re, im);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < S; j += 256) {
+    const double s = a.scales[j];
+    const double alpha = s * 2.0 * kPi / (N * a.dt);
+    const double c = sqrt(2.0 * kPi * s / a.dt) * 0.75112554446494248286 / N;
+    double2 w[2][8];
+    for (int which = 0; which < 2; ++which)
+      for (int t = 0; t < n0; ++t) {
+        double re = 0.0, im = 0.0;
+        for (int k = 0; k < N; ++k) {
+          const int kk = k < N / 2 ? k : k - N;
+          const double e = alpha * kk - a.f0;
+          const double psi = c * exp(-0.5 * e * e);
+          double sn, cs;
+          sincospi(2.0 * ((k * t) % N) / N, &sn, &cs);
+          const double2 x = X[which][k];
+          re += psi * (x.x * cs - x.y * sn);
+          im += psi * (x.x * sn + x.y * cs);
+        }
+        w[which][t] = make_double2(re, im);
+      }
+    // cross outputs and the three fields to smooth (zero past n0, as pycwt pads to N)
+    double z[4][8];
+    const long long rowbase = (b * S + j) * static_cast<long long>(n0);
+    for (int t = 0; t < n0; ++t) {
+      const double2 u = w[0][t], v = w[1][t];
+      const double wr = u.x * v.x + u.y * v.y, wi = u.y * v.x - u.x * v.y;  // W1 conj(W2)
+      const double pw = wr * wr + wi * wi;
+      if (a.out_pow) a.out_pow[rowbase + t] = static_cast<float>(pw);
+      if (a.out_sig) a.out_sig[rowbase + t] = static_cast<float>(atan2(wi, wr));  // phase plane
+      if (a.out_u) {
+        const double r = sqrt(pw);
+        a.out_u[rowbase + t] = r > 0 ? static_cast<float>(wi / r) : 0.f;
+        a.out_v[rowbase + t] = r > 0 ? static_cast<float>(wr / r) : 1.f;
+      }
+      z[0][t] = (u.x * u.x + u.y * u.y) / s;
+      z[1][t] = (v.x * v.x + v.y * v.y) / s;
+      z[2][t] = wr / s;
+      z[3][t] = wi / s;
+    }
+    // time Gaussian F(k) = exp(-(s/dt)^2 (2 pi kk / N)^2 / 2) by length-N DFTs
+    const double sg = s / a.dt * 2.0 * kPi / N;
+    double T[4][8];
+    for (int t = 0; t < n0; ++t) T[0][t] = T[1][t] = T[2][t] = T[3][t] = 0.0;
+    for (int k = 0; k < N; ++k) {
+      const int kk = k < N / 2 ? k : k - N;
+      const double F = exp(-0.5 * (sg * kk) * (sg * kk)) / N;
+      double Z[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // spectra of z1, z2 (real) and z12
+      for (int t = 0; t < n0; ++t) {
+        double sn, cs;
+        sincospi(-2.0 * ((k * t) % N) / N, &sn, &cs);
+        Z[0][0] += z[0][t] * cs;  Z[0][1] += z[0][t] * sn;
+        Z[1][0] += z[1][t] * cs;  Z[1][1] += z[1][t] * sn;
+        Z[2][0] += z[2][t] * cs - z[3][t] * sn;
+        Z[2][1] += z[2][t] * sn + z[3][t] * cs;
+      }
+      for (int t = 0; t < n0; ++t) {
+        double sn, cs;
+        sincospi(2.0 * ((k * t) % N) / N, &sn, &cs);
+        T[0][t] += F * (Z[0][0] * cs - Z[0][1] * sn);  // real parts: the smoothed real fields
+        T[1][t] += F * (Z[1][0] * cs - Z[1][1] * sn);
+        T[2][t] += F * (Z[2][0] * cs - Z[2][1] * sn);
+        T[3][t] += F * (Z[2][0] * sn + Z[2][1] * cs);
+      }
+    }
+    for (int t = 0; t < n0; ++t)
+      tsm[j * n0 + t] = make_float4(static_cast<float>(T[0][t]), static_cast<float>(T[1][t]),
+                                    static_cast<float>(T[2][t]), static_cast<float>(T[3][t]));
+  }
+  __syncthreads();
+  // scale boxcar (rows i - K/2 .. i + (K-1)/2, half weight at both ends) and the ratio
+  const int LO = K / 2;
+  const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
+  for (int idx = threadIdx.x; idx < S * n0; idx += 256) {
+    const int i = idx / n0, t = idx - i * n0;
+    float s1 = 0.f, s2 = 0.f, re = 0.f, im = 0.f;
+    for (int q = 0; q < K; ++q) {
+      const int row = i - LO + q;
+      if (row < 0 || row >= S) continue;
+      const float wq = (K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn;
+      const float4 v = tsm[row * n0 + t];
+      s1 = fmaf(wq, v.x, s1);
+      s2 = fmaf(wq, v.y, s2);
+      re = fmaf(wq, v.z, re);
+      im = fmaf(wq, v.w, im);
+    }
+    coh[(b * S + i) * static_cast<long long>(n0) + t] = (re * re + im * im) / (s1 * s2);
+  }
+}
+
 static int log2_ceil_w(long long n) {
   int l = 0;
   while ((1ll << l) < n) ++l;
@@ -840,6 +1008,7 @@ static long long wct_sb_bytes(long long batch, long long n0, int n_scales) {
 
 extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales) {
   if (batch < 0 || n0 < 0 || n_scales < 0) return -1;
+  if (n0 > (1 << 14)) return wct_long_workspace_bytes(batch, n0, n_scales);
   return wct_t_bytes(batch, n0, n_scales) + wct_spec_bytes(batch, n0) +
          wct_sb_bytes(batch, n0, n_scales) + 4ll * (3 * n_scales + 1);
 }
@@ -853,10 +1022,9 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
       ld < n0 || boxcar < 1)
     return kErrArg;
   if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
-  if (n0 > (1 << 14) || boxcar > 24) return kErrUnsupported;
+  if (n0 > (1ll << kLongMaxLog)) return kErrUnsupported;
   if (batch == 0 || n0 == 0 || n_scales == 0) return kOk;
   const int logn = log2_ceil_w(n0);
-  if (logn < 4) return kErrUnsupported;  // n0 <= 8: below the FFT engine's minimum row
   CwtArgs a{};
   a.x = x1;
   a.x2 = x2;
@@ -874,6 +1042,17 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   a.out_pow = out_power;
   a.out_sig = out_phase;  // phase-angle plane (atan2 of W12)
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (n0 > (1 << 14)) return wct_long(a, boxcar, workspace, out_coh, st);
+  if (logn < 4) {  // n0 <= 8: below the FFT engine's minimum row
+    const size_t lds = static_cast<size_t>(n_scales) * n0 * sizeof(float4);
+    if (lds > kWctDirectMaxLds || batch > 0x7fffffffll) return kErrUnsupported;
+    if (lds > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wct_direct_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipLaunchKernelGGL(wct_direct_kernel, dim3(static_cast<unsigned>(batch)), dim3(256), lds, st, a,
+                       1 << logn, boxcar, out_coh);
+    return launch_status();
+  }
   const long long plane = wct_t_bytes(batch, n0, n_scales) / 2;
   cpx* TA = static_cast<cpx*>(workspace);
   cpx* TB = reinterpret_cast<cpx*>(static_cast<char*>(workspace) + plane);
@@ -892,13 +1071,5 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
     default: return kErrUnsupported;
   }
   if (rc != kOk) return rc;
-  const int n0i = static_cast<int>(n0);
-  switch (boxcar) {
-#define WTMI_B(K) case K: return launch_phase_b<K>(TA, TB, batch, n0i, n_scales, out_coh, plan, st);
-    WTMI_B(1) WTMI_B(2) WTMI_B(3) WTMI_B(4) WTMI_B(5) WTMI_B(6) WTMI_B(7) WTMI_B(8)
-    WTMI_B(9) WTMI_B(10) WTMI_B(11) WTMI_B(12) WTMI_B(13) WTMI_B(14) WTMI_B(15) WTMI_B(16)
-    WTMI_B(17) WTMI_B(18) WTMI_B(19) WTMI_B(20) WTMI_B(21) WTMI_B(22) WTMI_B(23) WTMI_B(24)
-#undef WTMI_B
-    default: return kErrUnsupported;
-  }
+  return wct_phase_b_any(TA, TB, batch, static_cast<int>(n0), n_scales, out_coh, plan, boxcar, st);
 }

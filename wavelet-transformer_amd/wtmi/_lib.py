@@ -25,19 +25,22 @@ _U64 = C.c_ulonglong
 # name -> (restype, argtypes); mirrors include/wtmi.h exactly
 PROTOTYPES = {
     "wtmi_cwt_morlet": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _F64, _F64, _P, _I64, _P, _P,
-                               _P, _P]),
+                               _P, _P, _P]),
+    "wtmi_cwt_workspace_bytes": (_I64, [_I64, _I64, _I32, _I32]),
     "wtmi_xwt_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _P, _I64,
-                               _P, _P, _P, _P, _P, _P]),
+                               _P, _P, _P, _P, _P, _P, _P]),
     "wtmi_wct_workspace_bytes": (_I64, [_I64, _I64, _I32]),
     "wtmi_wct_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _I32,
                                _P, _P, _P, _P, _P, _P, _P]),
     "wtmi_rednoise": (_I32, [_P, _I64, _I64, _I64, _F64, _U64, _U64, _P]),
     "wtmi_coherence_histogram": (_I32, [_P, _I64, _I64, _I32, _P, _P, _I32, _I32, _P, _P]),
-    "wtmi_modwt": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _I32, _P, _P]),
-    "wtmi_imodwt": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _U64, _P, _I64, _P]),
+    "wtmi_modwt_workspace_bytes": (_I64, [_I64, _I64, _I32]),
+    "wtmi_modwt": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _I32, _P, _P, _P]),
+    "wtmi_imodwt": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _U64, _P, _I64, _P, _P]),
     "wtmi_dwt_lengths": (_I64, [_I64, _I32, _I32, _P]),
-    "wtmi_wavedec": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _I32, _P, _P]),
-    "wtmi_waverec": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _P]),
+    "wtmi_dwt_workspace_bytes": (_I64, [_I64, _I64, _I32, _I32]),
+    "wtmi_wavedec": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _I32, _P, _P, _P]),
+    "wtmi_waverec": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _P, _P]),
     "wtmi_series_moments": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P]),
     "wtmi_affine": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I64, _P]),
     "wtmi_set_option": (_I32, [C.c_char_p, _I64]),

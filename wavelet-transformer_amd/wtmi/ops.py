@@ -195,11 +195,27 @@ def cwt_morlet(x: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
         res["power"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
     if want_sig:
         res["sig"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
+    ws = _long_workspace(B, n0, S, 0, dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_cwt_morlet", _ptr(x), x.stride(0), B, n0, _ptr(aff), _ptr(sc), S,
                   float(dt), float(f0), _ptr(ss), sig_ld, _ptr(res.get("w")),
-                  _ptr(res.get("power")), _ptr(res.get("sig")), _stream(dev))
+                  _ptr(res.get("power")), _ptr(res.get("sig")), _ptr(ws), _stream(dev))
     return res
+
+
+MAX_SAMPLES = 1 << 20  # longest row the engine transforms (include/wtmi.h)
+
+
+def cwt_workspace_bytes(batch: int, n0: int, n_scales: int, pair: bool = False) -> int:
+    """Scratch bytes of a CWT / XWT launch (0 up to 16384 samples per row)."""
+    return int(_lib.call("wtmi_cwt_workspace_bytes", batch, n0, n_scales, int(pair)))
+
+
+def _long_workspace(B, n0, S, pair, dev):
+    if n0 > MAX_SAMPLES:
+        raise ValueError(f"series of {n0} samples: the engine transforms at most {MAX_SAMPLES}")
+    need = cwt_workspace_bytes(B, n0, S, bool(pair))
+    return torch.empty(need, dtype=torch.uint8, device=dev) if need > 0 else None
 
 
 def _pair_rows(x1, x2):
@@ -240,11 +256,12 @@ def xwt_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     if want_uv:
         res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
         res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
+    ws = _long_workspace(B, n0, S, 1, dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_xwt_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
                   _ptr(sc), S, float(dt), float(f0), _ptr(ss), sig_ld, _ptr(res.get("w12")),
                   _ptr(res.get("power")), _ptr(res.get("sig")), _ptr(res.get("u")),
-                  _ptr(res.get("v")), _stream(dev))
+                  _ptr(res.get("v")), _ptr(ws), _stream(dev))
     return res
 
 
@@ -263,6 +280,10 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     S = _n_scales(scales)
     _check_affine(affine1, B, "affine1")
     _check_affine(affine2, B, "affine2")
+    if n0 > MAX_SAMPLES:
+        raise ValueError(f"series of {n0} samples: the engine transforms at most {MAX_SAMPLES}")
+    if int(boxcar) < 1:
+        raise ValueError("boxcar must be >= 1")
     need = wct_workspace_bytes(B, n0, S)
     if workspace is not None and (not isinstance(workspace, torch.Tensor) or
                                   workspace.dtype != torch.uint8 or not workspace.is_contiguous()
@@ -348,10 +369,18 @@ def modwt(x: torch.Tensor, dec_lo, dec_hi, level: int, out: Optional[torch.Tenso
     B, n = x.shape
     lo, hi = _taps(dec_lo), _taps(dec_hi)
     w = _out(out, (B, level + 1, n), dev)
+    ws = _scratch(_lib.call("wtmi_modwt_workspace_bytes", B, n, int(level)), dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_modwt", _ptr(x), x.stride(0), B, n, lo.ctypes.data_as(VP),
-                  hi.ctypes.data_as(VP), lo.size, int(level), _ptr(w), _stream(dev))
+                  hi.ctypes.data_as(VP), lo.size, int(level), _ptr(w), _ptr(ws), _stream(dev))
     return w
+
+
+def _scratch(nbytes: int, dev):
+    """Device scratch of a long-series launch (None when the call needs none)."""
+    if nbytes < 0:
+        raise ValueError("invalid geometry")
+    return torch.empty(nbytes, dtype=torch.uint8, device=dev) if nbytes > 0 else None
 
 
 def imodwt(w: torch.Tensor, dec_lo, dec_hi, keep_mask: Optional[int] = None,
@@ -365,9 +394,10 @@ def imodwt(w: torch.Tensor, dec_lo, dec_hi, keep_mask: Optional[int] = None,
     lo, hi = _taps(dec_lo), _taps(dec_hi)
     keep = (1 << 64) - 1 if keep_mask is None else int(keep_mask)
     x = _out(out, (B, n), dev)
+    ws = _scratch(_lib.call("wtmi_modwt_workspace_bytes", B, n, R - 1), dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_imodwt", _ptr(w), B, n, lo.ctypes.data_as(VP), hi.ctypes.data_as(VP),
-                  lo.size, R - 1, C.c_ulonglong(keep), _ptr(x), x.stride(0), _stream(dev))
+                  lo.size, R - 1, C.c_ulonglong(keep), _ptr(x), x.stride(0), _ptr(ws), _stream(dev))
     return x
 
 
@@ -388,9 +418,10 @@ def wavedec(x: torch.Tensor, dec_lo, dec_hi, level: int):
     lo, hi = _taps(dec_lo), _taps(dec_hi)
     lens = dwt_lengths(n, lo.size, level)
     coeffs = torch.empty((B, sum(lens)), dtype=torch.float32, device=dev)
+    ws = _scratch(_lib.call("wtmi_dwt_workspace_bytes", B, n, lo.size, 1), dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_wavedec", _ptr(x), x.stride(0), B, n, lo.ctypes.data_as(VP),
-                  hi.ctypes.data_as(VP), lo.size, int(level), _ptr(coeffs), _stream(dev))
+                  hi.ctypes.data_as(VP), lo.size, int(level), _ptr(coeffs), _ptr(ws), _stream(dev))
     return coeffs, lens
 
 
@@ -409,10 +440,14 @@ def waverec(coeffs: torch.Tensor, n: int, rec_lo, rec_hi, level: int,
                                        dtype=np.uint64).view(np.int64), device=dev)
     B = coeffs.shape[0]
     out = torch.empty((B, len(keep_masks), out_len), dtype=torch.float32, device=dev)
+    if level == 0 and n > 16384:  # nothing to invert: the kept cA_0 is the series
+        keep = torch.tensor([float(int(m) & 1) for m in keep_masks], device=dev)
+        return coeffs[:, None, :n] * keep[None, :, None]
+    ws = _scratch(_lib.call("wtmi_dwt_workspace_bytes", B, n, lo.size, len(keep_masks)), dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_waverec", _ptr(coeffs), B, n, lo.ctypes.data_as(VP),
                   hi.ctypes.data_as(VP), lo.size, int(level), _ptr(masks), len(keep_masks),
-                  _ptr(out), out_len, _stream(dev))
+                  _ptr(out), out_len, _ptr(ws), _stream(dev))
     return out
 
 

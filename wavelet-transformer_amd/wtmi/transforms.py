@@ -399,6 +399,8 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     as pycwt's ``cache=True`` keeps them under the user cache dir (src/wct.py:117);
     ``seed`` None draws a fresh one, as pycwt's unseeded draws do."""
     wavelet = as_morlet(wavelet)
+    if wavelet.deltaj0 <= 0:
+        raise ValueError("wct_significance needs a Morlet(6) wavelet (deltaj0 defined)")
     key = ("wct_significance", 1, float(al1), float(al2), float(dt), float(dj), float(s0), int(J),
            float(significance_level), wavelet.f0, int(mc_count), int(nbins), seed)
     if cache:
@@ -406,6 +408,13 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
         if hit is not None:
             return hit
     N, sj, t_lo, t_hi, anyout, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
+    if N > ops.MAX_SAMPLES:
+        raise ValueError(f"wct_significance: noise length {N} exceeds the engine's "
+                         f"{ops.MAX_SAMPLES} samples per row")
+    # pairs per launch: the smoothed-row workspace is 16 B per (pair, scale, sample); keep a
+    # launch's workspace near 4 GiB for long noise rows
+    per_pair = max(1, ops.wct_workspace_bytes(1, N, sj.size))
+    max_pairs_per_launch = int(max(1, min(max_pairs_per_launch, (4 << 30) // per_pair)))
     if seed is None:
         seed = int(np.random.SeedSequence().entropy) & ((1 << 64) - 1)
     dev = device()
