@@ -186,5 +186,22 @@ def test_tiny_wct_matches_oracle(n0, dj):
     coh, aw, coi, freq, _ = transforms.wct(y1, y2, DT, dj=dj, s0=2 * DT, J=-1, sig=False)
     rc, ra, rcoi, rfreq, _ = pc.wct(y1, y2, DT, dj=dj, s0=2 * DT, J=-1, sig=False)
     assert coh.shape == rc.shape
-    assert np.abs(coh - rc).max() <= 1e-4
+    # n0 = 2: pycwt's normalisation sqrt(s * 2 pi fftfreq(2)[1] / dt * N) is the root of a
+    # negative number, every coefficient NaN; the engine returns the same NaNs
+    np.testing.assert_allclose(coh, rc, rtol=0, atol=1e-4, equal_nan=True)
+    assert np.isnan(coh).all() == (n0 == 2)
     np.testing.assert_allclose(freq, rfreq, rtol=1e-12)
+
+
+@pytest.mark.parametrize("n0", [2, 3, 5, 8])
+def test_tiny_cwt_matches_oracle(n0):
+    """n0 <= 8: the direct CWT kernel; n0 = 2 is all-NaN in pycwt (and here)."""
+    from wtmi import ops
+    rng = np.random.default_rng(100 + n0)
+    x = rng.standard_normal((2, n0)).astype(np.float32)
+    sj = _scales(n0, 1 / 8, 12)
+    W = ops.cwt_morlet(torch.tensor(x, device="cuda"), sj, DT)["w"].cpu().numpy()
+    for b in range(2):
+        ref = pc.cwt(x[b].astype(np.float64), DT, 1 / 8, 2 * DT, 12)[0]
+        np.testing.assert_allclose(W[b], ref, rtol=0, atol=1e-5 * np.nanmax(np.abs(ref), initial=1.0),
+                                   equal_nan=True)

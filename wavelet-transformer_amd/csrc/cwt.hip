@@ -243,7 +243,8 @@ __global__ void __launch_bounds__(256) cwt_direct_kernel(CwtArgs a, int N) {
   const long long b = rj / a.S;
   const double s = a.scales[j];
   const double alpha = s * 2.0 * kPi / (N * a.dt);
-  const double c = sqrt(2.0 * kPi * s / a.dt) * 0.75112554446494248286 / N;
+  // pycwt's sqrt(s * ftfreqs[1] * N): fftfreq(2)[1] = -1/2, so a 2-point row is NaN there too
+  const double c = N == 2 ? __builtin_nan("") : sqrt(2.0 * kPi * s / a.dt) * 0.75112554446494248286 / N;
   double2 w[2] = {make_double2(0, 0), make_double2(0, 0)};
   for (int which = 0; which < (MODE == 1 ? 2 : 1); ++which) {
     const float* row = (which ? a.x2 : a.x) + b * a.ld;

@@ -895,7 +895,9 @@ __global__ void __launch_bounds__(256) wct_direct_kernel(CwtArgs a, int N, int K
   for (int j = threadIdx.x; j < S; j += 256) {
     const double s = a.scales[j];
     const double alpha = s * 2.0 * kPi / (N * a.dt);
-    const double c = sqrt(2.0 * kPi * s / a.dt) * 0.75112554446494248286 / N;
+    // pycwt normalises by sqrt(s * ftfreqs[1] * N) with ftfreqs = 2 pi fftfreq(N) / dt: for
+    // N = 2, fftfreq(2)[1] = -1/2 and the reference's row is NaN -- kept
+    const double c = N == 2 ? __builtin_nan("") : sqrt(2.0 * kPi * s / a.dt) * 0.75112554446494248286 / N;
     double2 w[2][8];
     for (int which = 0; which < 2; ++which)
       for (int t = 0; t < n0; ++t) {
