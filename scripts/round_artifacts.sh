@@ -6,7 +6,7 @@
 #   3. bench.py per config (CPU baseline included)   -> gpurun_out/bench_<cfg>.json
 # Every GPU step has its own time limit; a crash / abort / timeout ends the session.
 set -u
-ROUND=${ROUND:-r01}
+ROUND=${ROUND:-r02}
 CFGS=${CFGS:-"c2 c3 c4 c5"}
 OUT=gpurun_out
 mkdir -p $OUT profiles/$ROUND
@@ -38,6 +38,7 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
 fi
 for c in $CFGS; do
   ARGS=""
+  [ $c = c2 ] && ARGS="--steps 20 --warmup 5"
   [ $c = c2 ] || ARGS="--steps 10 --warmup 3"
   run bench_$c 600 python bench.py --config $c $ARGS
   grep '^{' $OUT/bench_$c.log | tail -1 > $OUT/bench_$c.json

@@ -225,7 +225,7 @@ def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95, wavelet="mo
     x2 = ops.affine(d2, a2, torch.float32)
     W12 = ops.xwt_morlet(x1, x2, sj, dt, wavelet.f0, want_w12=True)["w12"][0]
     mh1, mh2 = _np(m1)[0], _np(m2)[0]
-    std1, std2 = (1.0, 1.0) if normalize else (mh1[1], mh2[1])
+    std1, std2 = mh1[1], mh2[1]  # raw series' std, normalised or not
     g1, _, _ = _ar1_from_moments(mh1[4], mh1[5], int(mh1[6]))
     g2, _, _ = _ar1_from_moments(mh2[4], mh2[5], int(mh2[6]))
     Pk1 = ar1_spectrum(freq * dt, g1)
