@@ -82,9 +82,11 @@ def test_wct_fused_power_and_phase_outputs(n, B):
 @pytest.mark.parametrize("n,dj", [(4096, 1 / 12), (8000, 1 / 8), (8192, 1 / 8), (3000, 1 / 16),
                                   (16384, 1 / 4)])
 def test_wct_band_paths_match_unpruned(n, dj):
-    """Band-pruned transforms, the spectral-correlation rows of phase A and phase C's
-    band-spectrum coherence against the unpruned path (six full transforms per row, every
-    output row through phase B).  Boxcar widths 14, 10, 19 and 5 rows; padded and full rows."""
+    """Band-pruned transforms, the spectral-correlation rows of phase A, the decimated spectra
+    of full rows (wct_prune 2: forward transforms on every (N/M)-th sample, band inverses of
+    M bins) and phase C's band-spectrum coherence against the unpruned path (six full
+    transforms per row, every output row through phase B).  Boxcar widths 14, 10, 19 and 5
+    rows; padded and full rows."""
     from wtmi import transforms
     rng = np.random.default_rng(n + 11)
     B = 2
@@ -93,17 +95,21 @@ def test_wct_band_paths_match_unpruned(n, dj):
     y2 = torch.tensor(np.stack([p[1] for p in pairs]), device="cuda", dtype=torch.float32)
     out = {}
     from wtmi import _lib
-    for prune in (0, 1):
+    for prune in (0, 1, 2):
         with _lib.option("wct_prune", prune):
             res, _, _ = transforms.wct_batch(y1, y2, 1 / 12, dj, 2 / 12, -1, want_uv=False,
                                              want_power=True, want_phase=True)
         out[prune] = {k: v.cpu().numpy().astype(np.float64) for k, v in res.items()}
-    full, band = out[0], out[1]
-    assert np.abs(full["coh"] - band["coh"]).max() <= 2e-5
-    assert row_relerr(band["power"], full["power"]).max() < 2e-5
-    mask = full["power"] > 1e-6 * full["power"].max(axis=-1, keepdims=True)
-    dphi = np.angle(np.exp(1j * (band["phase"] - full["phase"])))
-    assert np.abs(dphi[mask]).max() <= 1e-4
+    full = out[0]
+    # phases where |W12| > 1e-2 of its row's max: fp32 transforms leave |dW12| ~ 1e-6 of the
+    # row max in every path (the unpruned one included: 1.4e-4 rad against the fp64 oracle at
+    # 1e-3..1e-2 of the row max, scripts/debug/wct_phase_err.py), i.e. <= 1e-4 rad from there on
+    mask = full["power"] > 1e-4 * full["power"].max(axis=-1, keepdims=True)
+    for band in (out[1], out[2]):
+        assert np.abs(full["coh"] - band["coh"]).max() <= 2e-5
+        assert row_relerr(band["power"], full["power"]).max() < 2e-5
+        dphi = np.angle(np.exp(1j * (band["phase"] - full["phase"])))
+        assert np.abs(dphi[mask]).max() <= 1e-4
 
 
 def test_wct_batched_self_coherence_is_one():

@@ -104,9 +104,11 @@ enum : int {
 struct Options {
   int cwt_prune = 2;        // WTMI_CWT_PRUNE: 2 band rows + narrowed entry passes, 1 band rows, 0 full
   int cwt_target_wg = 0;    // WTMI_CWT_TARGET_WG: workgroups per CWT launch, 0 = by size
-  int wct_prune = 1;        // WTMI_WCT_PRUNE: 1 band-pruned WCT rows, 0 full
+  int wct_prune = 2;        // WTMI_WCT_PRUNE: 2 band rows + decimated spectra, 1 band rows, 0 full
   int wct_target_wg = 0;    // WTMI_WCT_TARGET_WG: 0 = as many as wct_min_rows allows
   int wct_min_rows = 4;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least
+  int wct_dec_rows = 4;     // WTMI_WCT_DEC_ROWS: decimated scale rows per phase A workgroup
+  int wct_overlap = 1;      // WTMI_WCT_OVERLAP: full-band WCT rows on a side stream (1) or in order (0)
 };
 const Options& options();
 

@@ -247,7 +247,36 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
 //   bit 4     spec  output row whose whole boxcar window has q >= 1: its coherence is made by
 //                   phase C from band spectra (no time-domain workspace round trip)
 //   bits 5-6  qw    that window's smallest regime (the union of the members' bands)
-enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5 };
+//   bits 8-11 e     decimation of the row (wct_dec_kernel), 0 = none: W1, W2 have their spectra in
+//                   bins [0, M/2), M = N >> e, so the products |W1|^2, W1 conj(W2) have theirs in
+//                   (-M/2, M/2) and the forward transforms run on every (N/M)-th sample (length M)
+enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5,
+             kPlanDecShift = 8 };
+__device__ __forceinline__ int plan_dec(int pl) { return (pl >> kPlanDecShift) & 15; }
+
+// Decimated rows: M = N >> e with e in [kDecMinE(LOGN), LOGN - 5] -- M >= 32 (the band
+// inverse's phasor is one per thread), M <= 4096 (256-thread decimated groups) -- for full rows
+// (n0 = N; a row truncated at n0 < N is not band-limited) of LOGN >= 10.
+template <int LOGN> __host__ __device__ constexpr int dec_min_e() { return LOGN - 12 > 1 ? LOGN - 12 : 1; }
+constexpr int kDecMinLogn = 10;
+constexpr int kDecMinLogm = 5;
+constexpr int kDecMaxLogm = 12;
+__host__ __device__ constexpr int dec_rows_per_wg(int logm) { return logm >= 12 ? 1 : 256 >> (logm - 4); }
+// schedule of wct_dec_kernel (after the plan's 3 S + 1 ints and S row-list ints):
+// [4 logm + 0] first row-list index, [+1] row count, [+2] first workgroup; [64] workgroups
+constexpr int kDecSched = 68;
+
+// e of row r (0: not decimated): the smallest M = 2^m >= 32 with psi negligible from bin M/2 on
+// (alpha M/2 - f0 >= kBandT, the band_regime criterion), if that M is at most N / 2.
+template <int LOGN>
+__device__ __forceinline__ int dec_e(double s, double dt, double f0) {
+  using P = FftPlan<LOGN>;
+  const double alpha = s * 2.0 * kPi / (static_cast<double>(P::N) * dt);
+  int lm = kDecMinLogm;
+  while (lm < LOGN && alpha * static_cast<double>(1 << (lm - 1)) - f0 < kBandT) ++lm;
+  const int e = LOGN - lm;
+  return (e >= dec_min_e<LOGN>() && e <= LOGN - kDecMinLogm) ? e : 0;
+}
 
 template <int LOGN>
 __device__ __forceinline__ int plan_q(const double* scales, int r, double dt, double f0) {
@@ -257,11 +286,12 @@ __device__ __forceinline__ int plan_q(const double* scales, int r, double dt, do
 }
 
 // One workgroup; plan[S] = last output row of phase B (the time path), -1 if none.
-// scratch: 2 S ints (row regimes, then each output row's window regime or -1).
+// scratch: 2 S ints (row regimes, then each output row's window regime or -1), then the
+// decimated rows' list (S ints) and schedule (kDecSched ints), see wct_dec_kernel.
 template <int LOGN>
 __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict__ scales, int S, double dt,
-                                                       double f0, int K, int prune, int* __restrict__ plan,
-                                                       int* __restrict__ scratch) {
+                                                       double f0, int K, int prune, int dec, long long batch,
+                                                       int* __restrict__ plan, int* __restrict__ scratch) {
   __shared__ int last;
   if (threadIdx.x == 0) last = -1;
   const int LO = K / 2, HI = (K - 1) / 2;
@@ -282,12 +312,41 @@ __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict_
       if (qwin[i] >= 1) needS = true; else needT = true;
     }
     const int qw = qwin[r];
+    const int e = dec ? dec_e<LOGN>(scales[r], dt, f0) : 0;
     plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
-              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0);
+              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) | (e << kPlanDecShift);
     if (qw < 1) atomicMax(&last, r);
   }
   __syncthreads();
-  if (threadIdx.x == 0) plan[S] = last;
+  // decimated rows by class (LDS counters; the order of rows within a class is immaterial)
+  __shared__ int cnt[16], cur[16];
+  if (threadIdx.x < 16) cnt[threadIdx.x] = cur[threadIdx.x] = 0;
+  __syncthreads();
+  for (int r = threadIdx.x; r < S; r += blockDim.x) {
+    const int e = plan_dec(plan[r]);
+    if (e > 0) atomicAdd(&cnt[LOGN - e], 1);
+  }
+  __syncthreads();
+  int* rows = scratch + 2 * S;
+  int* sched = rows + S;
+  if (threadIdx.x == 0) {
+    plan[S] = last;
+    int nlist = 0, wg = 0;
+    for (int lm = kDecMaxLogm; lm >= kDecMinLogm; --lm) {
+      sched[4 * lm + 0] = nlist;
+      sched[4 * lm + 1] = cnt[lm];
+      sched[4 * lm + 2] = wg;
+      cur[lm] = nlist;
+      nlist += cnt[lm];
+      wg += static_cast<int>((batch * cnt[lm] + dec_rows_per_wg(lm) - 1) / dec_rows_per_wg(lm));
+    }
+    sched[64] = wg;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < S; r += blockDim.x) {
+    const int e = plan_dec(plan[r]);
+    if (e > 0) rows[atomicAdd(&cur[LOGN - e], 1)] = r;
+  }
 }
 
 struct WctRowCtx {
@@ -299,10 +358,116 @@ struct WctRowCtx {
   cpx* TB;
   cpx* band;  // LDS: the band bins A1, A2 of a narrow row (2 * (N >> 8) complex)
   cpx* SB;    // smoothed band spectra [batch][S][2][NT] (index k + NT/2), see wct_plan
+  const cpx* DY;  // decimated rows: W12's spectrum [batch][S][N/2] (M bins, wct_dec_kernel)
   const int* plan;
   long long b;
   int j0;
 };
+
+// Full-length inverse transform of a spectrum held in bins k in [-M/2, M/2), M = N >> E, stored
+// in FFT order (bin k at k mod M) in global memory: the band is shifted by H = M/2 to [0, M),
+// transformed from the entry pass/width it allows (pass Q = E/4, inputs r < NZ = 16 >> E%4
+// non-zero: band_entry / the narrowed first pass), and the shift undone by the time phasor
+// exp(-2 pi i H n / N) (H a multiple of 16: one phasor per thread).  Split into the loads
+// (band_load) and the transform (band_ifft) so that callers issue the next transform's loads
+// before the current one's stores: loads and stores share one counter (vmcnt), so a load
+// issued after a row of stores waits for all of them.
+template <int LOGN, int E>
+struct BandGeom {
+  using P = FftPlan<LOGN>;
+  static constexpr int M = P::N >> E;
+  static constexpr int H = M / 2;
+  static constexpr int Q = E / 4;
+  static constexpr int NZ = 16 >> (E % 4);
+  static constexpr int NLD = Q == 0 ? NZ : 1;  // loads per thread
+  static_assert(M >= 32 && Q < P::P16, "band inverse");
+};
+
+template <int LOGN, int E>
+__device__ __forceinline__ void band_load(cpx (&pre)[8], const cpx* __restrict__ g, int t) {
+  using B = BandGeom<LOGN, E>;
+  using P = FftPlan<LOGN>;
+  if constexpr (B::Q == 0) {
+    // shifted bin t + r NT (< M) is bin t + r NT + H (r < NZ/2) or t + r NT - H of g
+    if constexpr (P::NT >= kWave) {  // rows are wave-aligned: buffer loads, offsets in SGPRs
+      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(g);
+#pragma unroll
+      for (int r = 0; r < B::NZ; ++r)
+        pre[r] = buf_ld_c64(rs, 8 * t, 8 * (r * P::NT + (r < B::NZ / 2 ? B::H : -B::H)));
+    } else {
+#pragma unroll
+      for (int r = 0; r < B::NZ; ++r) pre[r] = g[t + r * P::NT + (r < B::NZ / 2 ? B::H : -B::H)];
+    }
+  } else {
+    pre[0] = t < B::M ? g[(t + B::H) & (B::M - 1)] : mkc(0.f, 0.f);
+  }
+}
+
+template <int LOGN, int E, bool TWL>
+__device__ __forceinline__ void band_ifft(cpx (&v)[16], const cpx (&pre)[8], cpx* my, const cpx* tw, int t,
+                                          int& par, const float4* twl) {
+  using B = BandGeom<LOGN, E>;
+  using P = FftPlan<LOGN>;
+  if constexpr (B::Q == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = r < B::NZ ? pre[r] : mkc(0.f, 0.f);
+    fft_row<LOGN, 1, 1, TWL, 0, B::NZ>(v, my, 0, tw, t, par, twl);
+  } else {
+    band_entry<LOGN, B::Q, B::NZ>(v, pre[0], my, t);
+    fft_row<LOGN, 1, 1, TWL, B::Q, B::NZ>(v, my, 0, tw, t, par, twl);
+  }
+  int tt = t;
+  asm volatile("" : "+v"(tt));  // per row, not hoisted (register budget)
+  const cpx ph = expi_frac(-B::H * tt, P::N);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
+}
+
+// Phase A rows [r0, r1) of decimation e = E: the decimated spectra (wct_dec_kernel) hold W12's
+// whole spectrum and, for time-path rows, the smoothed fields' spectra in the rows' TA / TB
+// slots.  One band inverse gives W12 (power, phase, arrows); time-path rows add two more for
+// (T1, T2) and T12, written over the spectra they were made from.
+template <int LOGN, int E, bool TWL>
+__device__ __forceinline__ void wct_dec_rows(const CwtArgs& a, const WctRowCtx& c, int r0, int r1, cpx* my,
+                                             const cpx* tw, int g, int t, int& par, const float4* twl) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  constexpr bool BUF = P::NT >= kWave;
+  const int n0 = a.n0;
+  auto dy_row = [&](int r) {  // W12 spectrum of this group's row in the iteration at r
+    const int jl = r + g;
+    return c.DY + (c.b * a.S + c.j0 + (jl < r1 ? jl : r0)) * (P::N / 2);
+  };
+  cpx pre[8];
+  band_load<LOGN, E>(pre, dy_row(r0), t);
+  for (int r = r0; r < r1; r += G::ROWS) {
+    const int jl = r + g;
+    const bool valid = jl < r1;
+    const long long rowbase = (c.b * a.S + c.j0 + (valid ? jl : r0)) * static_cast<long long>(n0);
+    const bool more = r + G::ROWS < r1;  // uniform
+    int pl_any = 0;  // workgroup-uniform (the band inverses hold barriers)
+#pragma unroll
+    for (int gg = 0; gg < G::ROWS; ++gg)
+      if (r + gg < r1) pl_any |= c.plan[c.j0 + r + gg];
+    const bool tpath = pl_any & kPlanNeedT;
+    cpx v[16];
+    band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // W12
+    if (tpath)
+      band_load<LOGN, E>(pre, c.TA + rowbase, t);
+    else if (more)
+      band_load<LOGN, E>(pre, dy_row(r + G::ROWS), t);
+    if (valid) xwt_outputs<LOGN, BUF>(a, v, rowbase, t);
+    if (tpath) {
+      const bool wr = valid && (c.plan[c.j0 + (valid ? jl : r0)] & kPlanNeedT);
+      band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // (T1, T2)
+      band_load<LOGN, E>(pre, c.TB + rowbase, t);
+      if (wr) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // T12
+      if (more) band_load<LOGN, E>(pre, dy_row(r + G::ROWS), t);
+      if (wr) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return v[m]; });
+    }
+  }
+}
 
 // Phase A rows [r0, r1) of the workgroup's chunk, all of regime Q (one code path per loop:
 // branches between transform variants inside one loop cost the register allocator dearly).
@@ -438,10 +603,12 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
   }
 }
 
-template <int LOGN, bool FULL>
+// DEC: this launch runs the decimated rows (plan e > 0) only, else every other row (two
+// launches over the same chunk grid, so that each kernel gets its own register budget).
+template <int LOGN, bool FULL, bool DEC>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB,
-                cpx* __restrict__ SB, const int* __restrict__ plan) {
+                cpx* __restrict__ SB, const cpx* __restrict__ DY, const int* __restrict__ plan) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
   constexpr int BAND_F4 = LOGN >= 12 ? (P::N >> 8) : 1;  // 2 * (N >> 8) complex
@@ -461,14 +628,22 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   const int j0 = ch * a.chunk;
   const int j1 = min(a.S, j0 + a.chunk);
   cpx* my = lds + g * P::PADN;
+  {  // any rows of this launch's kind in the chunk?  (uniform: every thread reads the same plan)
+    bool any = false;
+    for (int r = j0; r < j1; ++r) any |= (plan_dec(plan[r]) > 0) == DEC;
+    if (!any) return;
+  }
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
+    const int pl = plan[j0 + i];
+    // run key: the regime, or 4 + e for decimated rows
+    q_tab[i] = plan_dec(pl) > 0 ? 4 + plan_dec(pl) : (pl & kPlanQ);
+    if (DEC) continue;  // decimated rows need no filter tables
     const double s = a.scales[j0 + i];
     prm_tab[i] = morlet_params(s, a.dt, P::N);
     const double sn = s / a.dt * 2.0 * kPi / P::N;  // (s/dt) * (2 pi / N)
     smt_tab[i] = mkc(static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn),
                      static_cast<float>(1.0 / (static_cast<double>(P::N) * s)));
-    q_tab[i] = plan[j0 + i] & kPlanQ;
   }
   constexpr bool TWL = G::TWL;
   cpx tw[TWL ? P::NTW_REG : P::NTW_ALLOC];
@@ -490,6 +665,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   c.TB = TB;
   c.band = reinterpret_cast<cpx*>(q_tab + G::MAXCHUNK);
   c.SB = SB;
+  c.DY = DY;
   c.plan = plan;
   c.b = b;
   c.j0 = j0;
@@ -500,7 +676,21 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     const int q = q_tab[r0];
     int r1 = r0 + 1;
     while (r1 < nrow && q_tab[r1] == q) ++r1;
-    if (q == 0) {
+    if (q >= 4) {  // decimated rows (full rows only)
+      if constexpr (DEC && FULL && LOGN >= kDecMinLogn) {
+        switch (q - 4) {
+#define WTMI_DR(EE)                                                                     \
+  case EE:                                                                              \
+    if constexpr (EE >= dec_min_e<LOGN>() && EE <= LOGN - kDecMinLogm)                  \
+      wct_dec_rows<LOGN, EE, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);                \
+    break;
+          WTMI_DR(1) WTMI_DR(2) WTMI_DR(3) WTMI_DR(4) WTMI_DR(5) WTMI_DR(6) WTMI_DR(7) WTMI_DR(8) WTMI_DR(9)
+#undef WTMI_DR
+          default: break;
+        }
+      }
+    } else if (DEC) {
+    } else if (q == 0) {
       if (a.prune && a.f0 >= kBandF0 && P::NT >= 16)  // negative frequencies dropped: half the bins
         wct_rows<LOGN, FULL, 0, TWL, 8>(a, c, r0, r1, my, tw, g, t, par, twl);
       else
@@ -519,6 +709,135 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     }
     r0 = r1;
   }
+}
+
+// Decimated spectra of the rows with plan e > 0 (full rows; M = N >> e, d = N / M):
+//   W1[d n'], W2[d n'] = inverse M-point transforms of the filtered spectra's bins [0, M/2)
+//     (the Morlet filter is negligible from bin M/2 on, and on the negative frequencies);
+//   z = |W1|^2 + i |W2|^2 and w = W1 conj(W2) at those M samples, forward M-point transforms:
+//     their spectra lie in (-M/2, M/2), so FFT_M(z[d n'])[k] = FFT_N(z)[k] / d exactly;
+//   out: Y = FFT_M(w) / M (W12's spectrum, DY row) for phase A's W12 outputs, and the smoothed
+//     Zs, Ys = F(k) FFT_M / (M s) (F the time Gaussian) to the band workspace SB (rows phase C
+//     reads) and / or, for time-path rows, in FFT order into the row's TA / TB slots.
+// Replaces, per row, two of phase A's forward N-point transforms by M-point ones, and its
+// inverse transforms by band inverses of M bins.  One 256-thread workgroup = 256 / (M/16)
+// (pair, row) items of one M (grid-stride over the schedule of wct_plan_kernel).  One
+// 512-thread workgroup = 256 / (M/16) items; an item is two thread groups of M/16 threads:
+// group f transforms W_f, the two swap through LDS, group 0 forward-transforms z and group 1 w.
+template <int LOGN, int LOGM>
+__device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restrict__ spec, cpx* __restrict__ TA,
+                                          cpx* __restrict__ TB, cpx* __restrict__ SB, cpx* __restrict__ DY,
+                                          const int* __restrict__ plan, const int* __restrict__ rows,
+                                          const int* __restrict__ sched, int wl, cpx* lds) {
+  using P = FftPlan<LOGN>;
+  using PM = FftPlan<LOGM>;
+  constexpr int ITEMS = dec_rows_per_wg(LOGM);
+  static_assert(2 * ITEMS * PM::NT == 512, "decimated workgroup");
+  constexpr int M = PM::N;
+  constexpr int NTM = PM::NT;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // per item: nothing (twiddles) hoisted out of the caller's loop
+  const int g = tid / NTM;  // thread group: item g / 2, field f = g & 1
+  const int f = g & 1;
+  const int t = tid - g * NTM;
+  const int first = sched[4 * LOGM], nr = sched[4 * LOGM + 1];
+  const long long item = static_cast<long long>(wl) * ITEMS + (g >> 1);
+  const bool valid = item < a.batch * nr;
+  const long long b = valid ? item / nr : 0;
+  const int j = rows[first + (valid ? static_cast<int>(item - b * nr) : 0)];
+  const int pl = plan[j];
+  cpx* my = lds + g * PM::PADN;
+  cpx tw[PM::NTW_ALLOC];
+  fft_twiddles<LOGM>(tw, t);
+  int par = 0;
+  const double s = a.scales[j];
+  const float f0 = static_cast<float>(a.f0);
+  cpx v[16];
+  {  // W_f at every d-th sample from bins t + m NTM (m < 8) of series f's spectrum
+    const cpx prm = morlet_params(s, a.dt, P::N);
+    const cpx* sp = spec + (2 * b + f) * static_cast<long long>(P::N);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = m < 8 ? sp[t + m * NTM] : mkc(0.f, 0.f);
+    morlet_filter_nz<LOGM, 8>(v, v, prm, f0, t);
+    fft_row<LOGM, 1, 1, false, 0, 8>(v, my, 0, tw, t, par);
+  }
+  // swap W1 / W2 between the item's two groups (positions t + m NTM, natural order)
+  __syncthreads();  // the transform's last reads of my are done
+#pragma unroll
+  for (int m = 0; m < 16; ++m) my[lpad(t + m * NTM)] = v[m];
+  __syncthreads();
+  {
+    const cpx* other = lds + (g ^ 1) * PM::PADN;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const cpx o = other[lpad(t + m * NTM)];
+      const cpx w1 = f == 0 ? v[m] : o, w2 = f == 0 ? o : v[m];
+      v[m] = f == 0 ? mkc(cabs2(w1), cabs2(w2)) : cmul(w1, cconj(w2));  // z / w
+    }
+  }
+  fft_row<LOGM, -1, 1, false>(v, my, 0, tw, t, par);
+  const long long row = b * a.S + j;
+  if (valid && f == 1) {  // W12's spectrum / M for phase A's W12 outputs
+    cpx* dy = DY + row * (P::N / 2);
+    constexpr float inv_m = 1.f / M;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) dy[t + m * NTM] = cscale(v[m], inv_m);
+  }
+  // smoothed band: F(k) / (M s); time-path rows -> TA / TB slot in FFT order, band rows -> SB
+  const double sn = s / a.dt * 2.0 * kPi / P::N;
+  const float beta = static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn);
+  const float sc = static_cast<float>(1.0 / (static_cast<double>(M) * s));
+  constexpr int NTN = P::NT;  // SB row: bins k in [-NTN/2, NTN/2) at k + NTN/2
+  const bool needT = valid && (pl & kPlanNeedT), needS = valid && (pl & kPlanNeedS);
+  cpx* trow = (f == 0 ? TA : TB) + row * static_cast<long long>(a.n0);
+  cpx* sb = SB + row * 2ll * NTN + f * NTN;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int k = t + (m < 8 ? m : m - 16) * NTM;
+    const float kk = static_cast<float>(k);
+    const cpx y = cscale(v[m], sc * __builtin_amdgcn_exp2f(beta * kk * kk));
+    if (needT) trow[t + m * NTM] = y;
+    if (needS && k >= -NTN / 2 && k < NTN / 2) sb[k + NTN / 2] = y;
+  }
+  if constexpr (M < NTN) {  // band rows' SB bins outside (-M/2, M/2): zero, by the whole workgroup
+    constexpr int Z = NTN - M;
+    for (int i = tid; i < ITEMS * 2 * Z; i += 2 * ITEMS * NTM) {
+      const int it = i / (2 * Z), rem = i - it * 2 * Z, ff = rem / Z, e = rem - ff * Z;
+      const long long item2 = static_cast<long long>(wl) * ITEMS + it;
+      if (item2 >= a.batch * nr) break;
+      const long long b2 = item2 / nr;
+      const int j2 = rows[first + static_cast<int>(item2 - b2 * nr)];
+      if (plan[j2] & kPlanNeedS)
+        SB[(b2 * a.S + j2) * 2ll * NTN + ff * NTN + (e < NTN / 2 - M / 2 ? e : e + M)] = mkc(0.f, 0.f);
+    }
+  }
+}
+
+// One launch per decimation class (the class sizes are known on the device only: each launch
+// covers the largest possible class, workgroups past the schedule's count exit at once).
+template <int LOGN, int LOGM>
+__global__ void __launch_bounds__(512, 4) wct_dec_kernel(CwtArgs a, const cpx* __restrict__ spec,
+                                                         cpx* __restrict__ TA, cpx* __restrict__ TB,
+                                                         cpx* __restrict__ SB, cpx* __restrict__ DY,
+                                                         const int* __restrict__ plan) {
+  __shared__ cpx lds[2 * dec_rows_per_wg(LOGM) * FftPlan<LOGM>::PADN];
+  const int* rows = plan + 3 * a.S + 1;
+  const int* sched = rows + a.S;
+  const int w0 = sched[4 * LOGM + 2];
+  const int nwg = (LOGM > kDecMinLogm ? sched[4 * (LOGM - 1) + 2] : sched[64]) - w0;
+  if (static_cast<int>(blockIdx.x) < nwg) dec_items<LOGN, LOGM>(a, spec, TA, TB, SB, DY, plan, rows, sched, blockIdx.x, lds);
+}
+
+template <int LOGN, int LOGM>
+static int launch_dec_class(const CwtArgs& a, const cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY,
+                            const int* plan, hipStream_t st) {
+  if constexpr (LOGM >= kDecMinLogm && LOGM <= LOGN - dec_min_e<LOGN>()) {
+    // the class's workgroups are at most this many; the surplus exits at once
+    const unsigned dg = static_cast<unsigned>((a.batch * a.S + dec_rows_per_wg(LOGM) - 1) / dec_rows_per_wg(LOGM));
+    hipLaunchKernelGGL((wct_dec_kernel<LOGN, LOGM>), dim3(dg), dim3(512), 0, st, a, spec, TA, TB, SB, DY, plan);
+    return launch_status();
+  }
+  return kOk;
 }
 
 // Scale boxcar + coherence.  Row i uses rows i - K/2 .. i + (K-1)/2 (zero outside),
@@ -751,9 +1070,37 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   }
 }
 
+// Side stream (per device, created at first use) on which the WCT runs its full-band rows'
+// kernel beside the decimated rows' work; fork / join by events, so the pair stays
+// capturable in a hipGraph with the caller's stream.
+struct SideStream {
+  hipStream_t s;
+  hipEvent_t fork, join;
+};
+static SideStream* side_stream(hipStream_t st) {
+  static SideStream res[16];
+  static bool ready[16];
+  int dev = 0;
+  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (dev < 0 || dev >= 16) return nullptr;
+  if (!ready[dev]) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(dev) != hipSuccess) return nullptr;
+    SideStream r{};
+    const bool ok = hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking) == hipSuccess &&
+                    hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&r.join, hipEventDisableTiming) == hipSuccess;
+    (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
+    res[dev] = r;
+    ready[dev] = true;
+  }
+  return &res[dev];
+}
+
 template <int LOGN>
-static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int* plan, int K,
-                          float* coh, hipStream_t st) {
+static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY, int* plan, int K,
+                          float* coh, hipStream_t st, SideStream* side, bool& joined) {
   using G = WctGeom<LOGN>;
   {
     const long long items = 2 * a.batch;
@@ -783,17 +1130,55 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, int*
   a.chunk = chunk;
   a.prune = options().wct_prune;
   const long long grid = a.batch * nch;
-  if (grid > 0x7fffffffll) return kErrUnsupported;
+  if (grid > 0x7fffffffll || a.batch * a.S > 0x7fffffffll - 64) return kErrUnsupported;
+  // decimated rows: full rows, pruning level 2, Morlet negative frequencies negligible
+  const int dec = (a.prune >= 2 && a.n0 == (1 << LOGN) && LOGN >= kDecMinLogn && a.f0 >= kBandF0) ? 1 : 0;
   hipLaunchKernelGGL(wct_plan_kernel<LOGN>, dim3(1), dim3(256), 0, st, a.scales, a.S, a.dt, a.f0, K,
-                     a.prune, plan, plan + a.S + 1);
+                     a.prune, dec, a.batch, plan, plan + a.S + 1);
   int rc = launch_status();
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
-  if (a.n0 == (1 << LOGN))
-    hipLaunchKernelGGL((wct_phase_a<LOGN, true>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, plan);
-  else
-    hipLaunchKernelGGL((wct_phase_a<LOGN, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, plan);
-  return launch_status();
+  joined = true;
+  if (a.n0 != (1 << LOGN)) {
+    hipLaunchKernelGGL((wct_phase_a<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, plan);
+    return launch_status();
+  }
+  // Full rows.  With decimated rows, the other rows' kernel (FFT-bound, rows of small scale)
+  // runs on a side stream beside the decimated spectra, the decimated rows' kernel (store-
+  // bound) and phase C (which reads only decimated rows' band spectra then); the caller
+  // joins before phase B.
+  hipStream_t fs = st;
+  if (dec && side) {
+    if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+      return launch_status();
+    fs = side->s;
+    joined = false;
+  }
+  hipLaunchKernelGGL((wct_phase_a<LOGN, true, false>), gd, dim3(G::BLOCK), 0, fs, a, spec, TA, TB, SB, DY, plan);
+  if ((rc = launch_status()) != kOk) return rc;
+  if (!joined && hipEventRecord(side->join, fs) != hipSuccess) return launch_status();
+  if constexpr (LOGN >= kDecMinLogn) {
+    if (dec) {
+      for (int lm = kDecMaxLogm; lm >= kDecMinLogm; --lm) {
+        switch (lm) {
+#define WTMI_DC(LM) case LM: rc = launch_dec_class<LOGN, LM>(a, spec, TA, TB, SB, DY, plan, st); break;
+          WTMI_DC(12) WTMI_DC(11) WTMI_DC(10) WTMI_DC(9) WTMI_DC(8) WTMI_DC(7) WTMI_DC(6) WTMI_DC(5)
+#undef WTMI_DC
+          default: break;
+        }
+        if (rc != kOk) return rc;
+      }
+      // decimated rows cost one to three band inverses each: chunks of their own length
+      CwtArgs ad = a;
+      ad.chunk = ((options().wct_dec_rows + rows - 1) / rows) * rows;
+      if (ad.chunk > G::MAXCHUNK) ad.chunk = G::MAXCHUNK;
+      ad.nchunks = (a.S + ad.chunk - 1) / ad.chunk;
+      hipLaunchKernelGGL((wct_phase_a<LOGN, true, true>), dim3(static_cast<unsigned>(a.batch * ad.nchunks)),
+                         dim3(G::BLOCK), 0, st, ad, spec, TA, TB, SB, DY, plan);
+      return launch_status();
+    }
+  }
+  return kOk;
 }
 
 // Phase C over the chunk grid phase A used (a.nchunks / a.chunk as launch_phase_a set them).
@@ -1002,7 +1387,9 @@ static int log2_ceil_w(long long n) {
 using namespace wtmi;
 
 // workspace = [T: batch x S x n0 float4][spectra: batch x 2 x N cpx]
-//             [band spectra: batch x S x 2 x N/16 cpx][plan: S + 1 int][plan scratch: 2 S int]
+//             [band spectra: batch x S x 2 x N/16 cpx][decimated W12 spectra: batch x S x N/2 cpx,
+//             N >= 2^kDecMinLogn][plan: S + 1 int][plan scratch: 2 S int][decimated rows: S int]
+//             [decimated schedule: kDecSched int]
 static long long wct_t_bytes(long long batch, long long n0, int n_scales) {
   const long long b = batch * n0 * static_cast<long long>(n_scales) * static_cast<long long>(sizeof(cpx));
   return 2 * ((b + 255) & ~255ll);
@@ -1015,12 +1402,16 @@ static long long wct_sb_bytes(long long batch, long long n0, int n_scales) {
   const long long nt = wct_n(n0) / 16 > 0 ? wct_n(n0) / 16 : 1;
   return (batch * n_scales * 2 * nt * static_cast<long long>(sizeof(cpx)) + 255) & ~255ll;
 }
+static long long wct_dy_bytes(long long batch, long long n0, int n_scales) {
+  if (wct_n(n0) < (1ll << kDecMinLogn) || wct_n(n0) != n0) return 0;  // decimated rows: full rows only
+  return (batch * n_scales * (wct_n(n0) / 2) * static_cast<long long>(sizeof(cpx)) + 255) & ~255ll;
+}
 
 extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int n_scales) {
   if (batch < 0 || n0 < 0 || n_scales < 0) return -1;
   if (n0 > (1 << 14)) return wct_long_workspace_bytes(batch, n0, n_scales);
-  return wct_t_bytes(batch, n0, n_scales) + wct_spec_bytes(batch, n0) +
-         wct_sb_bytes(batch, n0, n_scales) + 4ll * (3 * n_scales + 1);
+  return wct_t_bytes(batch, n0, n_scales) + wct_spec_bytes(batch, n0) + wct_sb_bytes(batch, n0, n_scales) +
+         wct_dy_bytes(batch, n0, n_scales) + 4ll * (4 * n_scales + 1 + kDecSched);
 }
 
 extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
@@ -1071,10 +1462,14 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   ws += wct_spec_bytes(batch, n0);
   cpx* SB = reinterpret_cast<cpx*>(ws);
   ws += wct_sb_bytes(batch, n0, n_scales);
+  cpx* DY = reinterpret_cast<cpx*>(ws);  // used only when wct_dy_bytes > 0 (launch_phase_a's dec)
+  ws += wct_dy_bytes(batch, n0, n_scales);
   int* plan = reinterpret_cast<int*>(ws);
   int rc;
+  SideStream* side = options().wct_overlap ? side_stream(st) : nullptr;
+  bool joined = true;
   switch (logn) {
-#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, plan, boxcar, out_coh, st); break;
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, plan, boxcar, out_coh, st, side, joined); break;
     WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
     WTMI_A(12) WTMI_A(13) WTMI_A(14)
 #undef WTMI_A
@@ -1094,5 +1489,6 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   // (phase B on a side stream beside phase C, fork/join by events, measured no faster:
   // C4 4.21-4.36 vs 4.23-4.24 ms -- phase C's workgroups hold the CUs, r02)
   if ((rc = phase_c(st)) != kOk) return rc;
+  if (!joined && hipStreamWaitEvent(st, side->join, 0) != hipSuccess) return launch_status();
   return wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st);
 }
