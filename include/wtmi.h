@@ -143,7 +143,7 @@ int wtmi_affine(const void* x, int x_is_f64, long long ld_in, long long batch, l
  * Launch-policy knobs, read from WTMI_<NAME> environment variables once at first use
  * and settable here: cwt_prune (2 band rows + narrowed entry passes, 1 band rows, 0 full
  * transforms), cwt_target_wg, wct_prune (2 band rows + decimated spectra of full rows, 1 band
- * rows, 0 full transforms), wct_target_wg, wct_min_rows, wct_dec_rows, wct_overlap (1: the
+ * rows, 0 full transforms), wct_target_wg, wct_min_rows, wct_dec_rows, wct_d_seg, wct_overlap (1: the
  * WCT's full-band rows on a library-owned side stream, fork/join by events).  The prune
  * switches exist so that tests can compare pruned and full transforms; results agree
  * to fp32 resolution either way.  Not thread-safe against concurrent launches.
