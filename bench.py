@@ -319,7 +319,9 @@ class C4(Workload):
     """XWT + WCT: 512 pairs x 8192, dj = 1/8 -> 97 scales."""
     name, axis, seed = "c4", "pair", 1004
     B, n, dj = 512, 8192, 1 / 8
-    kernel = "wct_plan<13>+wct_spectra<13>+wct_phase_a<13>+wct_phase_c<13>+wct_phase_b<10>"
+    kernel = ("moments<float> x2 + wct_spectra<13> + wct_plan<13> + wct_phase_a<13,full-band rows> (side stream) || "
+              "wct_dec_kernel<13,5..12> + wct_phase_d<13> + wct_phase_a<13,decimated rows> + wct_phase_c<13>; "
+              "wct_phase_b<10>")
 
     def setup(self):
         from wtmi import transforms
@@ -334,8 +336,7 @@ class C4(Workload):
         self.bytes = self.units * 12 + self.local * self.n * 8
         self.ws = torch.empty(self.ops.wct_workspace_bytes(max(self.local, 1), self.n, S),
                               dtype=torch.uint8, device=dev)
-        self.per_step = {"wtmi::wct_plan_kernel<": 1, "wtmi::wct_spectra<": 1, "wtmi::wct_phase_a<": 1,
-                         "wtmi::wct_phase_c<": 1, "wtmi::wct_phase_b<": 1}
+        self.per_step = {"wtmi::wct_": 1, "wtmi::moments_kernel<": 2}
         self.bytes_note = "12 B/coeff (|W12|^2 + WCT + phase, f32) + 8 B/pair-sample inputs"
 
     def step(self):
@@ -404,11 +405,11 @@ def pmc_traffic(cfg, per_step):
         if not ent:
             continue
         total, seen = 0.0, 0
-        for prefix, count in per_step.items():
+        for prefix, count in per_step.items():  # every kernel of the prefix, `count` launches each
             hits = [v for k, v in ent["kernels"].items() if k.startswith(prefix)]
-            if len(hits) != 1:
+            if not hits:
                 break
-            total += hits[0]["hbm_bytes"] * count
+            total += sum(h["hbm_bytes"] for h in hits) * count
             seen += 1
         if seen == len(per_step):
             return total, os.path.relpath(path, ROOT)

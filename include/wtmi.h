@@ -138,12 +138,19 @@ int wtmi_series_moments(const void* x, int x_is_f64, long long ld, long long bat
                         double* out, void* stream);
 int wtmi_affine(const void* x, int x_is_f64, long long ld_in, long long batch, long long n,
                 const double* coef, void* y, int y_is_f64, long long ld_out, void* stream);
+/* The affine coefficients [batch][3] (a0, a1, a2: x' = (x - a0 - a1 t) a2) in one pass over the
+ * series, for the transforms' `affine` arguments: mode bits 1 detrend (polyfit deg 1), 2 remove
+ * the mean, 4 divide by the std -- standardize_series(detrend, standardize, remove_mean) of
+ * src/utils/wavelet_helpers.py:22-57 (1 and 2 together: -1, as its ValueError), and 6 = pycwt's
+ * xwt/wct normalisation (y - mean) / std.  moments: [batch][8] as above, or NULL. */
+int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batch, long long n, int mode,
+                       double* moments, double* affine, void* stream);
 
 /* ---- launch options (no reference counterpart) ----------------------------------
  * Launch-policy knobs, read from WTMI_<NAME> environment variables once at first use
  * and settable here: cwt_prune (2 band rows + narrowed entry passes, 1 band rows, 0 full
  * transforms), cwt_target_wg, wct_prune (2 band rows + decimated spectra of full rows, 1 band
- * rows, 0 full transforms), wct_target_wg, wct_min_rows, wct_dec_rows, wct_d_seg, wct_overlap (1: the
+ * rows, 0 full transforms), wct_target_wg, wct_min_rows, wct_dec_rows, wct_overlap (1: the
  * WCT's full-band rows on a library-owned side stream, fork/join by events).  The prune
  * switches exist so that tests can compare pruned and full transforms; results agree
  * to fp32 resolution either way.  Not thread-safe against concurrent launches.

@@ -139,6 +139,18 @@ def test_moments_and_standardize_match_numpy():
                                        gs.standardize_series(x, **kw), rtol=1e-9, atol=1e-9)
     with pytest.raises(ValueError):
         transforms.standardize_series(x, detrend=True, remove_mean=True)
+    # the one-pass affine coefficients (wtmi_series_affine) == the moments-derived ones
+    xs = torch.tensor(rng.standard_normal((3, 777)).cumsum(1) + 50, device="cuda")
+    mom = ops.series_moments(xs)
+    for det, std, rm in ((True, True, False), (False, True, True), (False, True, False), (True, False, False)):
+        mode = (ops.AFF_DETREND if det else 0) | (ops.AFF_STANDARDIZE if std else 0) | \
+            (ops.AFF_REMOVE_MEAN if rm else 0)
+        torch.testing.assert_close(ops.series_affine(xs, mode),
+                                   transforms.standardize_coefs(mom, det, std, rm), rtol=1e-14, atol=0)
+    torch.testing.assert_close(ops.series_affine(xs.float()), transforms.normalize_coefs(ops.series_moments(xs.float())),
+                               rtol=1e-14, atol=0)
+    with pytest.raises(ValueError):
+        ops.series_affine(xs, ops.AFF_DETREND | ops.AFF_REMOVE_MEAN)
 
 
 def test_ar1_and_cpi_fallback_warning():

@@ -20,7 +20,6 @@ constexpr Entry kEntries[] = {
     {"wct_min_rows", &Options::wct_min_rows, 1, 1 << 10},
     {"wct_dec_rows", &Options::wct_dec_rows, 1, 128},
     {"wct_overlap", &Options::wct_overlap, 0, 1},
-    {"wct_d_seg", &Options::wct_d_seg, 1, 1 << 10},
 };
 
 Options& mutable_options() {
@@ -47,7 +46,7 @@ const Options& options() { return mutable_options(); }
 }  // namespace wtmi
 
 // Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
-// wct_min_rows, wct_dec_rows, wct_overlap, wct_d_seg).  0 on success, -1 unknown name or out of range.  Applies to launches
+// wct_min_rows, wct_dec_rows, wct_overlap).  0 on success, -1 unknown name or out of range.  Applies to launches
 // issued after the call; not to be called while another thread is launching.
 extern "C" int wtmi_set_option(const char* name, long long value) {
   if (!name) return wtmi::kErrArg;

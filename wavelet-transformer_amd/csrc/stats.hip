@@ -28,11 +28,16 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
   return r;
 }
 
+// Affine modes (wtmi_series_affine): the [B][3] coefficients (a0, a1, a2) of x' = (x - a0 - a1 t) a2
+// that standardize_series / the pycwt normalisation apply, straight from the moments.
+enum : int { kAffDetrend = 1, kAffRemoveMean = 2, kAffStandardize = 4 };
+
 // out[b*8 + {0..7}] = mean, std (ddof 0), slope, intercept (least squares vs
-// t = 0..n-1), c0 = sum((x-m)^2)/n, c1 = sum((x_i-m)(x_{i+1}-m))/(n-1), n, 0
+// t = 0..n-1), c0 = sum((x-m)^2)/n, c1 = sum((x_i-m)(x_{i+1}-m))/(n-1), n, 0 (out may be null);
+// aff[b*3 + {0..2}] = the affine coefficients of `mode` (aff may be null)
 template <typename T>
 __global__ void __launch_bounds__(kStatThreads) moments_kernel(const void* x, long long ld, int n,
-                                                               double* out) {
+                                                               double* out, int mode, double* aff) {
   __shared__ double sh[kStatThreads / 64];
   const long long b = blockIdx.x;
   const long long base = b * ld;
@@ -53,15 +58,24 @@ __global__ void __launch_bounds__(kStatThreads) moments_kernel(const void* x, lo
   if (threadIdx.x == 0) {
     const double stt = static_cast<double>(n) * (static_cast<double>(n) * n - 1.0) / 12.0;
     const double slope = stt > 0 ? sxt / stt : 0.0;
-    double* o = out + 8 * b;
-    o[0] = mean;
-    o[1] = sqrt(sxx / n);
-    o[2] = slope;
-    o[3] = mean - slope * tbar;
-    o[4] = sxx / n;
-    o[5] = n > 1 ? sl1 / (n - 1) : 0.0;
-    o[6] = n;
-    o[7] = 0.0;
+    const double sd = sqrt(sxx / n);
+    if (out) {
+      double* o = out + 8 * b;
+      o[0] = mean;
+      o[1] = sd;
+      o[2] = slope;
+      o[3] = mean - slope * tbar;
+      o[4] = sxx / n;
+      o[5] = n > 1 ? sl1 / (n - 1) : 0.0;
+      o[6] = n;
+      o[7] = 0.0;
+    }
+    if (aff) {  // as transforms.standardize_coefs / normalize_coefs (detrend wins over the mean)
+      double* c = aff + 3 * b;
+      c[0] = (mode & kAffDetrend) ? mean - slope * tbar : ((mode & kAffRemoveMean) ? mean : 0.0);
+      c[1] = (mode & kAffDetrend) ? slope : 0.0;
+      c[2] = (mode & kAffStandardize) ? 1.0 / sd : 1.0;
+    }
   }
 }
 
@@ -83,19 +97,32 @@ __global__ void __launch_bounds__(256) affine_kernel(const void* x, long long ld
 
 using namespace wtmi;
 
-extern "C" int wtmi_series_moments(const void* x, int x_is_f64, long long ld, long long batch,
-                                   long long n, double* out, void* stream) {
-  if (!x || !out || batch < 0 || n < 1 || ld < n || n > 0x7fffffff) return kErrArg;
+static int launch_moments(const void* x, int x_is_f64, long long ld, long long batch, long long n, double* out,
+                          int mode, double* aff, void* stream) {
   if (batch == 0) return kOk;
   if (batch > 0x7fffffffll) return kErrUnsupported;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (x_is_f64)
     hipLaunchKernelGGL(moments_kernel<double>, dim3(batch), dim3(kStatThreads), 0, st, x, ld,
-                       static_cast<int>(n), out);
+                       static_cast<int>(n), out, mode, aff);
   else
     hipLaunchKernelGGL(moments_kernel<float>, dim3(batch), dim3(kStatThreads), 0, st, x, ld,
-                       static_cast<int>(n), out);
+                       static_cast<int>(n), out, mode, aff);
   return launch_status();
+}
+
+extern "C" int wtmi_series_moments(const void* x, int x_is_f64, long long ld, long long batch,
+                                   long long n, double* out, void* stream) {
+  if (!x || !out || batch < 0 || n < 1 || ld < n || n > 0x7fffffff) return kErrArg;
+  return launch_moments(x, x_is_f64, ld, batch, n, out, 0, nullptr, stream);
+}
+
+extern "C" int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batch, long long n,
+                                  int mode, double* moments, double* affine, void* stream) {
+  if (!x || !affine || batch < 0 || n < 1 || ld < n || n > 0x7fffffff || mode < 0 || mode > 7 ||
+      ((mode & kAffDetrend) && (mode & kAffRemoveMean)))
+    return kErrArg;
+  return launch_moments(x, x_is_f64, ld, batch, n, moments, mode, affine, stream);
 }
 
 extern "C" int wtmi_affine(const void* x, int x_is_f64, long long ld_in, long long batch, long long n,

@@ -250,12 +250,8 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
 //   bits 8-11 e     decimation of the row (wct_dec_kernel), 0 = none: W1, W2 have their spectra in
 //                   bins [0, M/2), M = N >> e, so the products |W1|^2, W1 conj(W2) have theirs in
 //                   (-M/2, M/2) and the forward transforms run on every (N/M)-th sample (length M)
-//   bit 12    dw    output row whose window holds decimated rows only, some of them full-band
-//                   regime: its coherence is made by phase D (wct_phase_d) from their spectra
-//   bit 13    needZ the row's smoothed spectra stay in its TA / TB slots for phase D
 enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5,
-             kPlanDecShift = 8, kPlanDW = 1 << 12, kPlanNeedZ = 1 << 13 };
-constexpr int kPhaseDMinLogn = 12;  // phase D: one row per workgroup (FftPlan NT >= 256)
+             kPlanDecShift = 8 };
 __device__ __forceinline__ int plan_dec(int pl) { return (pl >> kPlanDecShift) & 15; }
 
 // Decimated rows: M = N >> e with e in [kDecMinE(LOGN), LOGN - 5] -- M >= 32 (the band
@@ -265,6 +261,9 @@ template <int LOGN> __host__ __device__ constexpr int dec_min_e() { return LOGN 
 constexpr int kDecMinLogn = 10;
 constexpr int kDecMinLogm = 5;
 constexpr int kDecMaxLogm = 12;
+// the decimated transforms run at M_eng = max(M, 2^kDecEngLogm): rows of smaller M share one
+// launch (their bins past M/2 are dropped on store)
+constexpr int kDecEngLogm = 8;
 __host__ __device__ constexpr int dec_rows_per_wg(int logm) { return logm >= 12 ? 1 : 256 >> (logm - 4); }
 // schedule of wct_dec_kernel (after the plan's 3 S + 1 ints and S row-list ints):
 // [4 logm + 0] first row-list index, [+1] row count, [+2] first workgroup; [64] workgroups
@@ -304,29 +303,22 @@ __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict_
   for (int r = threadIdx.x; r < S; r += blockDim.x)
     qrow[r] = (prune ? plan_q<LOGN>(scales, r, dt, f0) : 0) | ((dec ? dec_e<LOGN>(scales[r], dt, f0) : 0) << 4);
   __syncthreads();
-  // window regime; -1: some member has q = 0 (time path), -2: phase D (all members decimated)
-  const bool dwok = dec && LOGN >= kPhaseDMinLogn;
-  for (int i = threadIdx.x; i < S; i += blockDim.x) {
+  for (int i = threadIdx.x; i < S; i += blockDim.x) {  // window regime; -1: some member has q = 0
     int qw = 3;
-    bool alld = true;
-    for (int r = max(0, i - LO); r <= min(S - 1, i + HI); ++r) {
-      qw = min(qw, qrow[r] & 15);
-      alld = alld && (qrow[r] >> 4) > 0;
-    }
-    qwin[i] = (prune && qw >= 1) ? qw : (dwok && alld ? -2 : -1);
+    for (int r = max(0, i - LO); r <= min(S - 1, i + HI); ++r) qw = min(qw, qrow[r] & 15);
+    qwin[i] = (prune && qw >= 1) ? qw : -1;
   }
   __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
     const int q = qrow[r] & 15, e = qrow[r] >> 4;
-    bool needT = false, needS = false, needZ = false;
+    bool needT = false, needS = false;
     for (int i = max(0, r - HI); i <= min(S - 1, r + LO); ++i) {  // outputs whose window holds r
-      if (qwin[i] >= 1) needS = true; else if (qwin[i] == -2) needZ = true; else needT = true;
+      if (qwin[i] >= 1) needS = true; else needT = true;
     }
     const int qw = qwin[r];
     plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
-              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) | (e << kPlanDecShift) |
-              (qw == -2 ? kPlanDW : 0) | (needZ ? kPlanNeedZ : 0);
-    if (qw == -1) atomicMax(&last, r);
+              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) | (e << kPlanDecShift);
+    if (qw < 1) atomicMax(&last, r);
   }
   __syncthreads();
   // decimated rows by class (LDS counters; the order of rows within a class is immaterial)
@@ -335,7 +327,7 @@ __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict_
   __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
     const int e = plan_dec(plan[r]);
-    if (e > 0) atomicAdd(&cnt[LOGN - e], 1);
+    if (e > 0) atomicAdd(&cnt[max(LOGN - e, kDecEngLogm)], 1);
   }
   __syncthreads();
   int* rows = scratch + 2 * S;
@@ -343,7 +335,7 @@ __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict_
   if (threadIdx.x == 0) {
     plan[S] = last;
     int nlist = 0, wg = 0;
-    for (int lm = kDecMaxLogm; lm >= kDecMinLogm; --lm) {
+    for (int lm = kDecMaxLogm; lm >= kDecEngLogm; --lm) {
       sched[4 * lm + 0] = nlist;
       sched[4 * lm + 1] = cnt[lm];
       sched[4 * lm + 2] = wg;
@@ -356,7 +348,7 @@ __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict_
   __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
     const int e = plan_dec(plan[r]);
-    if (e > 0) rows[atomicAdd(&cur[LOGN - e], 1)] = r;
+    if (e > 0) rows[atomicAdd(&cur[max(LOGN - e, kDecEngLogm)], 1)] = r;
   }
 }
 
@@ -788,18 +780,27 @@ __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restric
   }
   fft_row<LOGM, -1, 1, false>(v, my, 0, tw, t, par);
   const long long row = b * a.S + j;
+  const int mr = P::N >> plan_dec(pl);  // the row's own M (<= M): bins |k| < mr/2 are stored
+  auto keep = [&](int m, int& ix) {     // FFT-order index of this thread's bin m in the row's M
+    const int k = t + (m < 8 ? m : m - 16) * NTM;
+    ix = k & (mr - 1);
+    return M == mr || (k >= -mr / 2 && k < mr / 2);
+  };
   if (valid && f == 1) {  // W12's spectrum / M for phase A's W12 outputs
     cpx* dy = DY + row * (P::N / 2);
     constexpr float inv_m = 1.f / M;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) dy[t + m * NTM] = cscale(v[m], inv_m);
+    for (int m = 0; m < 16; ++m) {
+      int ix;
+      if (keep(m, ix)) dy[ix] = cscale(v[m], inv_m);
+    }
   }
   // smoothed band: F(k) / (M s); time-path rows -> TA / TB slot in FFT order, band rows -> SB
   const double sn = s / a.dt * 2.0 * kPi / P::N;
   const float beta = static_cast<float>(-0.5 * 1.44269504088896340736 * sn * sn);
   const float sc = static_cast<float>(1.0 / (static_cast<double>(M) * s));
   constexpr int NTN = P::NT;  // SB row: bins k in [-NTN/2, NTN/2) at k + NTN/2
-  const bool needT = valid && (pl & (kPlanNeedT | kPlanNeedZ)), needS = valid && (pl & kPlanNeedS);
+  const bool needT = valid && (pl & kPlanNeedT), needS = valid && (pl & kPlanNeedS);
   cpx* trow = (f == 0 ? TA : TB) + row * static_cast<long long>(a.n0);
   cpx* sb = SB + row * 2ll * NTN + f * NTN;
 #pragma unroll
@@ -807,7 +808,8 @@ __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restric
     const int k = t + (m < 8 ? m : m - 16) * NTM;
     const float kk = static_cast<float>(k);
     const cpx y = cscale(v[m], sc * __builtin_amdgcn_exp2f(beta * kk * kk));
-    if (needT) trow[t + m * NTM] = y;
+    int ix;
+    if (needT && keep(m, ix)) trow[ix] = y;
     if (needS && k >= -NTN / 2 && k < NTN / 2) sb[k + NTN / 2] = y;
   }
   if constexpr (M < NTN) {  // band rows' SB bins outside (-M/2, M/2): zero, by the whole workgroup
@@ -835,14 +837,14 @@ __global__ void __launch_bounds__(512, 4) wct_dec_kernel(CwtArgs a, const cpx* _
   const int* rows = plan + 3 * a.S + 1;
   const int* sched = rows + a.S;
   const int w0 = sched[4 * LOGM + 2];
-  const int nwg = (LOGM > kDecMinLogm ? sched[4 * (LOGM - 1) + 2] : sched[64]) - w0;
+  const int nwg = (LOGM > kDecEngLogm ? sched[4 * (LOGM - 1) + 2] : sched[64]) - w0;
   if (static_cast<int>(blockIdx.x) < nwg) dec_items<LOGN, LOGM>(a, spec, TA, TB, SB, DY, plan, rows, sched, blockIdx.x, lds);
 }
 
 template <int LOGN, int LOGM>
 static int launch_dec_class(const CwtArgs& a, const cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY,
                             const int* plan, hipStream_t st) {
-  if constexpr (LOGM >= kDecMinLogm && LOGM <= LOGN - dec_min_e<LOGN>()) {
+  if constexpr (LOGM >= kDecEngLogm && LOGM <= LOGN - dec_min_e<LOGN>()) {
     // the class's workgroups are at most this many; the surplus exits at once
     const unsigned dg = static_cast<unsigned>((a.batch * a.S + dec_rows_per_wg(LOGM) - 1) / dec_rows_per_wg(LOGM));
     hipLaunchKernelGGL((wct_dec_kernel<LOGN, LOGM>), dim3(dg), dim3(512), 0, st, a, spec, TA, TB, SB, DY, plan);
@@ -905,7 +907,7 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
 #pragma unroll
     for (int r = 0; r < K; ++r) {
       const int i = jb + r - HI;
-      fl[r] = (i >= 0 && i < S) ? plan[i] : kPlanSpec;  // spec / dw rows: not the time path
+      fl[r] = (i >= 0 && i < S) ? plan[i] : kPlanSpec;
     }
 #pragma unroll
     for (int r = 0; r < K; ++r) {
@@ -930,7 +932,7 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
         for (int f = 0; f < F; ++f) ra[r][f] = rb[r][f] = 0.f;
       }
       const int i = j - HI;
-      if (i >= 0 && i < S && !(fl[r] & (kPlanSpec | kPlanDW))) {
+      if (i >= 0 && i < S && !(fl[r] & kPlanSpec)) {
         float acc[2][F] = {};
 #pragma unroll
         for (int q = 0; q < K; ++q) {
@@ -1081,137 +1083,6 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   }
 }
 
-// Phase D: coherence of the output rows whose window holds decimated rows only, some of them of
-// the full-band regime (plan bit kPlanDW) -- the rows phase B would otherwise take from the
-// time-domain workspace.  The scale boxcar is applied to the rows' smoothed spectra (kept by
-// wct_dec_kernel in FFT order in their TA / TB slots, M = N >> e bins each), in the band
-// band [-M/2, M/2) of the widest decimated row (M = N >> dec_min_e): a running weighted sum down the scale
-// axis, S_i = S_{i-1} + (Z_{i+HI-1} + Z_{i+HI} - Z_{i-LO-1} - Z_{i-LO}) / 2 (end weights 1/2),
-// rebuilt every 8 rows, then two band inverses (S1 + i S2 and S12) and WCT = |S12|^2/(S1 S2).
-// A workgroup walks wct_d_seg (option) consecutive phase-D rows of one pair (4 spectrum rows of <= N/2
-// bins read per output row instead of the 2 x 16 B per coefficient the time path writes and
-// reads back).
-// az, ay += w x row rr's Z / Y spectra on this thread's bins of the band [-H, H) of layout E
-// (band_load's: Q = 0 -> bins t + r NT - H, r < NZ; Q >= 1 -> bin t - H, t < M); bins outside the
-// row's own band |k| < M_rr / 2 are zero and not loaded.  Rows outside [0, S): nothing.
-template <int LOGN, int E>
-__device__ __forceinline__ void dband_add(cpx (&az)[8], cpx (&ay)[8], const cpx* __restrict__ TA,
-                                          const cpx* __restrict__ TB, const int* __restrict__ plan, long long base,
-                                          int n0, int S, int rr, float w, int t) {
-  using B = BandGeom<LOGN, E>;
-  using P = FftPlan<LOGN>;
-  if (rr < 0 || rr >= S) return;
-  const int mh = P::N >> (plan_dec(plan[rr]) + 1);  // the row's M / 2
-  const long long off = (base + rr) * static_cast<long long>(n0);
-  const cpx ww = cpx{w, w};
-  const cpx* z = TA + off;
-  const cpx* y = TB + off;
-#pragma unroll
-  for (int r = 0; r < B::NLD; ++r) {
-    const int k = (B::Q == 0 ? t + r * P::NT : t) - B::H;
-    const bool in = (B::Q == 0 || t < B::M) && k >= -mh && k < mh;
-    const int ix = in ? (k & (2 * mh - 1)) : 0;
-    const cpx zz = z[ix], yy = y[ix];
-    az[r] = in ? cfma(ww, zz, az[r]) : az[r];
-    ay[r] = in ? cfma(ww, yy, ay[r]) : ay[r];
-  }
-}
-
-// Output rows [i0, i1) of one pair (the phase-D rows among them), band layout E.
-template <int LOGN, int E, bool TWL>
-__device__ __forceinline__ void phase_d_rows(int S, int n0, const cpx* __restrict__ TA, const cpx* __restrict__ TB,
-                                             const int* __restrict__ plan, int K, long long b, int i0, int i1,
-                                             float* __restrict__ coh, cpx* my, const cpx* tw, int t,
-                                             const float4* twl) {
-  using P = FftPlan<LOGN>;
-  constexpr bool BUF = P::NT >= kWave;
-  int par = 0;
-  const int LO = K / 2, HI = (K - 1) / 2;
-  const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
-  const long long base = b * S;
-// (one row's loads at a time: all four rows' in flight at once need 128 VGPRs)
-#define WTMI_DADD(RR, W)                                                                   \
-  do {                                                                                     \
-    dband_add<LOGN, E>(bz, by, TA, TB, plan, base, n0, S, (RR), (W), t);                   \
-    asm volatile("" ::: "memory");                                                         \
-  } while (0)
-  cpx bz[8], by[8];  // the weighted window sums of the Z and Y spectra
-  int run = 0;  // rows since the sums were rebuilt (0: rebuild)
-  for (int i = i0; i < i1; ++i) {
-    if (!(plan[i] & kPlanDW)) {
-      run = 0;
-      continue;
-    }
-    if (run == 0 || run >= 8) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) bz[r] = by[r] = mkc(0.f, 0.f);
-      for (int q = 0; q < K; ++q) WTMI_DADD(i - LO + q, (K > 1 && (q == 0 || q == K - 1)) ? 0.5f : 1.f);
-      run = 0;
-    } else if (K > 1) {  // window i - 1 -> i: the end weights move one row down
-      WTMI_DADD(i - LO - 1, -0.5f);
-      WTMI_DADD(i - LO, -0.5f);
-      WTMI_DADD(i + HI - 1, 0.5f);
-      WTMI_DADD(i + HI, 0.5f);
-    } else {
-      WTMI_DADD(i - 1, -1.f);
-      WTMI_DADD(i, 1.f);
-    }
-#undef WTMI_DADD
-    ++run;
-    cpx pre[8], v[16];
-    float den[16];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) pre[r] = bz[r] * wn;
-    band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // S1 + i S2
-#pragma unroll
-    for (int m = 0; m < 16; ++m) den[m] = v[m].x * v[m].y;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) pre[r] = by[r] * wn;
-    band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // S12 (|S12|^2 is phasor-free; applied anyway)
-    put_row<LOGN, BUF>(coh + (base + i) * static_cast<long long>(n0), t, n0,
-                       [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
-  }
-}
-
-template <int LOGN>
-__global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
-    wct_phase_d(CwtArgs a, const cpx* __restrict__ TA, const cpx* __restrict__ TB, const int* __restrict__ plan,
-                int K, int seglen, float* __restrict__ coh) {
-  using P = FftPlan<LOGN>;
-  using G = WctGeom<LOGN>;
-  static_assert(G::ROWS == 1, "phase D: one row per workgroup");
-  __shared__ float4 lds4[P::PADN / 2 + G::TWL_F4];
-  cpx* my = reinterpret_cast<cpx*>(lds4);
-  float4* twl = lds4 + P::PADN / 2;
-  const int t = threadIdx.x;
-  const int S = a.S;
-  const int nseg = (S + seglen - 1) / seglen;
-  const long long b = blockIdx.x / nseg;
-  const int seg = static_cast<int>(blockIdx.x - b * nseg);
-  // this workgroup's rows: the phase-D rows of rank [seg L, seg L + L) (uniform scan)
-  int i0 = -1, i1 = -1, rank = 0;
-  for (int i = 0; i < S; ++i) {
-    if (!(plan[i] & kPlanDW)) continue;
-    if (rank == seg * seglen) i0 = i;
-    if (rank < (seg + 1) * seglen) i1 = i + 1;
-    ++rank;
-  }
-  if (i0 < 0) return;
-  // one band layout for every segment: the widest a decimated row can have (M = N >> dec_min_e);
-  // a row's bins outside its own band are not loaded (the transforms' width differs little:
-  // phase-D windows reach the full-band regime, M >= N/8 at their widest row)
-  constexpr bool TWL = G::TWL;
-  cpx tw[TWL ? P::NTW_REG : P::NTW_ALLOC];
-  if constexpr (TWL) {
-    fft_twiddle_table<LOGN>(twl, t, G::BLOCK);
-    fft_twiddles_tail<LOGN>(tw, t);
-  } else {
-    fft_twiddles<LOGN>(tw, t);
-  }
-  __syncthreads();
-  phase_d_rows<LOGN, dec_min_e<LOGN>(), TWL>(S, a.n0, TA, TB, plan, K, b, i0, i1, coh, my, tw, t, twl);
-}
-
 // Side stream (per device, created at first use) on which the WCT runs its full-band rows'
 // kernel beside the decimated rows' work; fork / join by events, so the pair stays
 // capturable in a hipGraph with the caller's stream.
@@ -1301,22 +1172,14 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   if (!joined && hipEventRecord(side->join, fs) != hipSuccess) return launch_status();
   if constexpr (LOGN >= kDecMinLogn) {
     if (dec) {
-      for (int lm = kDecMaxLogm; lm >= kDecMinLogm; --lm) {
+      for (int lm = kDecMaxLogm; lm >= kDecEngLogm; --lm) {
         switch (lm) {
 #define WTMI_DC(LM) case LM: rc = launch_dec_class<LOGN, LM>(a, spec, TA, TB, SB, DY, plan, st); break;
-          WTMI_DC(12) WTMI_DC(11) WTMI_DC(10) WTMI_DC(9) WTMI_DC(8) WTMI_DC(7) WTMI_DC(6) WTMI_DC(5)
+          WTMI_DC(12) WTMI_DC(11) WTMI_DC(10) WTMI_DC(9) WTMI_DC(8)
 #undef WTMI_DC
           default: break;
         }
         if (rc != kOk) return rc;
-      }
-      // phase D reads the spectra the decimated phase A then turns into time-domain rows
-      if constexpr (LOGN >= kPhaseDMinLogn) {
-        const int seglen = options().wct_d_seg;
-        const long long dgrid = a.batch * ((a.S + seglen - 1) / seglen);  // surplus segments exit
-        hipLaunchKernelGGL(wct_phase_d<LOGN>, dim3(static_cast<unsigned>(dgrid)), dim3(G::BLOCK), 0, st, a, TA,
-                           TB, plan, K, seglen, coh);
-        if ((rc = launch_status()) != kOk) return rc;
       }
       // decimated rows cost one to three band inverses each: chunks of their own length
       CwtArgs ad = a;
@@ -1373,7 +1236,7 @@ __global__ void __launch_bounds__(256) wct_phase_b_generic(const cpx* __restrict
   const long long base = b * static_cast<long long>(S) * n0 + u;
   const int last = plan[S];
   for (int i = 0; i <= last && i < S; ++i) {
-    if (plan[i] & (kPlanSpec | kPlanDW)) continue;
+    if (plan[i] & kPlanSpec) continue;
     float s1 = 0.f, s2 = 0.f, re = 0.f, im = 0.f;
     for (int q = 0; q < K; ++q) {
       const int row = i - LO + q;

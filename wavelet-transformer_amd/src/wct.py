@@ -89,8 +89,8 @@ def run_wct(wavelet_coherence_transform: Type[DataForWCT], calculate_signficance
         raise AssertionError("Input signals must have the same size")
     d1 = transforms._to_dev(y1).reshape(1, -1)
     d2 = transforms._to_dev(y2).reshape(1, -1)
-    x1 = ops.affine(d1, transforms.normalize_coefs(ops.series_moments(d1)), torch.float32)
-    x2 = ops.affine(d2, transforms.normalize_coefs(ops.series_moments(d2)), torch.float32)
+    x1 = ops.affine(d1, ops.series_affine(d1, ops.AFF_NORMALIZE), torch.float32)
+    x2 = ops.affine(d2, ops.series_affine(d2, ops.AFF_NORMALIZE), torch.float32)
     res, sj, freqs = transforms.wct_batch(x1, x2, d.delta_t, d.delta_j, d.initial_scale, -1, mother,
                                           normalize=False, want_uv=True)
     n0 = y1.size

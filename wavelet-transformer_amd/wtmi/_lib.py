@@ -42,6 +42,7 @@ PROTOTYPES = {
     "wtmi_wavedec": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _I32, _P, _P, _P]),
     "wtmi_waverec": (_I32, [_P, _I64, _I64, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _P, _P]),
     "wtmi_series_moments": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P]),
+    "wtmi_series_affine": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _P, _P, _P]),
     "wtmi_affine": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I64, _P]),
     "wtmi_set_option": (_I32, [C.c_char_p, _I64]),
     "wtmi_get_option": (_I64, [C.c_char_p]),

@@ -100,6 +100,26 @@ def series_moments(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+AFF_DETREND, AFF_REMOVE_MEAN, AFF_STANDARDIZE = 1, 2, 4
+AFF_NORMALIZE = AFF_REMOVE_MEAN | AFF_STANDARDIZE  # pycwt xwt / wct: (y - mean) / std
+
+
+def series_affine(x: torch.Tensor, mode: int = AFF_NORMALIZE) -> torch.Tensor:
+    """[B, 3] float64 affine coefficients (x - a0 - a1 t) * a2 from one moments pass (mode bits:
+    1 detrend, 2 remove mean, 4 standardize; 1 and 2 together raise ValueError)."""
+    if (mode & AFF_DETREND) and (mode & AFF_REMOVE_MEAN):
+        raise ValueError("Only standardize by either removing secular trend or mean, not both.")
+    x = _rows(x)
+    dev = _check_dev(x)
+    if x.dtype not in (torch.float32, torch.float64):
+        x = x.to(torch.float64)
+    out = torch.empty((x.shape[0], 3), dtype=torch.float64, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_series_affine", _ptr(x), int(x.dtype == torch.float64), x.stride(0),
+                  x.shape[0], x.shape[1], int(mode), None, _ptr(out), _stream(dev))
+    return out
+
+
 def affine(x: torch.Tensor, coef: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
     """y = (x - a0 - a1 t) * a2 per series (coef [B, 3] float64), computed in fp64."""
     x = _rows(x)

@@ -156,7 +156,8 @@ def normalize_coefs(mom: torch.Tensor) -> torch.Tensor:
 def standardize_series_dev(y: torch.Tensor, detrend=True, standardize=True, remove_mean=False,
                            dtype=torch.float64) -> torch.Tensor:
     y = y if y.dim() == 2 else y.reshape(1, -1)
-    coef = standardize_coefs(ops.series_moments(y), detrend, standardize, remove_mean)
+    coef = ops.series_affine(y, (ops.AFF_DETREND if detrend else 0) | (ops.AFF_REMOVE_MEAN if remove_mean else 0)
+                             | (ops.AFF_STANDARDIZE if standardize else 0))
     return ops.affine(y, coef, dtype)
 
 
@@ -250,8 +251,8 @@ def wct_batch(y1: torch.Tensor, y2: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wa
     sj, freqs = scales_for(n0, dt, dj, s0, J, wavelet)
     a1 = a2 = None
     if normalize:
-        a1 = normalize_coefs(ops.series_moments(y1))
-        a2 = normalize_coefs(ops.series_moments(y2))
+        a1 = ops.series_affine(y1, ops.AFF_NORMALIZE)
+        a2 = ops.series_affine(y2, ops.AFF_NORMALIZE)
     res = ops.wct_morlet(y1, y2, sj, dt, wavelet.f0, boxcar=boxcar_rows(wavelet, dj), affine1=a1,
                          affine2=a2, want_uv=want_uv, want_power=want_power,
                          want_phase=want_phase, workspace=workspace)
@@ -444,7 +445,7 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
 
 def _norm32(d: torch.Tensor) -> torch.Tensor:
     """(y - mean) / std in fp64 on the device, rounded once to fp32."""
-    return ops.affine(d, normalize_coefs(ops.series_moments(d)), torch.float32)
+    return ops.affine(d, ops.series_affine(d, ops.AFF_NORMALIZE), torch.float32)
 
 
 # ------------------------------------------------------------------------- DWT
