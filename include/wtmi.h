@@ -150,8 +150,8 @@ int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batc
  * Launch-policy knobs, read from WTMI_<NAME> environment variables once at first use
  * and settable here: cwt_prune (2 band rows + narrowed entry passes, 1 band rows, 0 full
  * transforms), cwt_target_wg, wct_prune (2 band rows + decimated spectra of full rows, 1 band
- * rows, 0 full transforms), wct_target_wg, wct_min_rows, wct_dec_rows, wct_overlap (1: the
- * WCT's full-band rows on a library-owned side stream, fork/join by events).  The prune
+ * rows, 0 full transforms), wct_target_wg, wct_min_rows, wct_dec_rows (decimated scale rows per
+ * WCT phase-A workgroup).  The prune
  * switches exist so that tests can compare pruned and full transforms; results agree
  * to fp32 resolution either way.  Not thread-safe against concurrent launches.
  * wtmi_set_option: 0, or -1 for an unknown name / out-of-range value;

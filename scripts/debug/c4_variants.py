@@ -24,7 +24,6 @@ def run(**kw):
 
 variants = [("pow+phase", dict(want_power=True, want_phase=True), {}),
             ("coh only", dict(), {}),
-            ("pow+phase overlap 0", dict(want_power=True, want_phase=True), {"wct_overlap": 0}),
             ("pow+phase dec_rows 8", dict(want_power=True, want_phase=True), {"wct_dec_rows": 8}),
             ("pow+phase prune 1", dict(want_power=True, want_phase=True), {"wct_prune": 1})]
 for rep in range(2):

@@ -108,7 +108,6 @@ struct Options {
   int wct_target_wg = 0;    // WTMI_WCT_TARGET_WG: 0 = as many as wct_min_rows allows
   int wct_min_rows = 4;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least
   int wct_dec_rows = 4;     // WTMI_WCT_DEC_ROWS: decimated scale rows per phase A workgroup
-  int wct_overlap = 1;      // WTMI_WCT_OVERLAP: full-band WCT rows on a side stream (1) or in order (0)
 };
 const Options& options();
 

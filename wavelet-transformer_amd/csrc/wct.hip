@@ -1083,37 +1083,9 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   }
 }
 
-// Side stream (per device, created at first use) on which the WCT runs its full-band rows'
-// kernel beside the decimated rows' work; fork / join by events, so the pair stays
-// capturable in a hipGraph with the caller's stream.
-struct SideStream {
-  hipStream_t s;
-  hipEvent_t fork, join;
-};
-static SideStream* side_stream(hipStream_t st) {
-  static SideStream res[16];
-  static bool ready[16];
-  int dev = 0;
-  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) return nullptr;
-  if (dev < 0 || dev >= 16) return nullptr;
-  if (!ready[dev]) {
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(dev) != hipSuccess) return nullptr;
-    SideStream r{};
-    const bool ok = hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking) == hipSuccess &&
-                    hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) == hipSuccess &&
-                    hipEventCreateWithFlags(&r.join, hipEventDisableTiming) == hipSuccess;
-    (void)hipSetDevice(cur);
-    if (!ok) return nullptr;
-    res[dev] = r;
-    ready[dev] = true;
-  }
-  return &res[dev];
-}
-
 template <int LOGN>
 static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY, int* plan, int K,
-                          float* coh, hipStream_t st, SideStream* side, bool& joined) {
+                          float* coh, hipStream_t st) {
   using G = WctGeom<LOGN>;
   {
     const long long items = 2 * a.batch;
@@ -1151,25 +1123,15 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   int rc = launch_status();
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
-  joined = true;
   if (a.n0 != (1 << LOGN)) {
     hipLaunchKernelGGL((wct_phase_a<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, plan);
     return launch_status();
   }
-  // Full rows.  With decimated rows, the other rows' kernel (FFT-bound, rows of small scale)
-  // runs on a side stream beside the decimated spectra, the decimated rows' kernel (store-
-  // bound) and phase C (which reads only decimated rows' band spectra then); the caller
-  // joins before phase B.
-  hipStream_t fs = st;
-  if (dec && side) {
-    if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
-      return launch_status();
-    fs = side->s;
-    joined = false;
-  }
-  hipLaunchKernelGGL((wct_phase_a<LOGN, true, false>), gd, dim3(G::BLOCK), 0, fs, a, spec, TA, TB, SB, DY, plan);
+  // Full rows: the non-decimated rows' kernel, then (with decimated rows) their spectra and their
+  // kernel.  (Running the first on a second stream beside the decimated work, and phase C beside
+  // the decimated rows' kernel, measured a tie and 0.1 ms slower on C4: each saturates the CUs.)
+  hipLaunchKernelGGL((wct_phase_a<LOGN, true, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, plan);
   if ((rc = launch_status()) != kOk) return rc;
-  if (!joined && hipEventRecord(side->join, fs) != hipSuccess) return launch_status();
   if constexpr (LOGN >= kDecMinLogn) {
     if (dec) {
       for (int lm = kDecMaxLogm; lm >= kDecEngLogm; --lm) {
@@ -1479,10 +1441,8 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   ws += wct_dy_bytes(batch, n0, n_scales);
   int* plan = reinterpret_cast<int*>(ws);
   int rc;
-  SideStream* side = options().wct_overlap ? side_stream(st) : nullptr;
-  bool joined = true;
   switch (logn) {
-#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, plan, boxcar, out_coh, st, side, joined); break;
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, plan, boxcar, out_coh, st); break;
     WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
     WTMI_A(12) WTMI_A(13) WTMI_A(14)
 #undef WTMI_A
@@ -1502,6 +1462,5 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   // (phase B on a side stream beside phase C, fork/join by events, measured no faster:
   // C4 4.21-4.36 vs 4.23-4.24 ms -- phase C's workgroups hold the CUs, r02)
   if ((rc = phase_c(st)) != kOk) return rc;
-  if (!joined && hipStreamWaitEvent(st, side->join, 0) != hipSuccess) return launch_status();
   return wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st);
 }
