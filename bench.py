@@ -511,9 +511,12 @@ def main():
     sync()
     extra = 0
     while time.perf_counter() - t_warm < args.prewarm_s:
-        wl.step()
+        # back-to-back steps (a sync per 16): a host sync after every step left the GPU idle
+        # between them, and the timed region then opened below the loaded clock
+        for _ in range(16):
+            wl.step()
         sync()
-        extra += 1
+        extra += 16
     barrier()
     sync()
 
