@@ -518,7 +518,10 @@ __global__ void __launch_bounds__(T, 1)
   auto chain_log = [&](int dm) {
     if ((dm & 3) == 0 && NG == ng && (NG & (NG - 1)) == 0) {
       const int dq = dm >> 2;
-      if (dq > 0 && (dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) return __builtin_ctz(dq);
+      // chains from dq = 2 groups: at dq = 1 the chain lanes stride 128 B and every load
+      // instruction touches 64 lines; the stride form's coalesced loads win there (C3 A/B on
+      // one box: 2.82 -> 2.79 ms; chains from dq 4: 2.85, from 8: 2.93)
+      if (dq >= 2 && (dq & (dq - 1)) == 0 && ng % (GROUPS * dq) == 0) return __builtin_ctz(dq);
     }
     return -1;
   };
