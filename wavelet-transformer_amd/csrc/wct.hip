@@ -1,4 +1,4 @@
-// Wavelet coherence (K7 + K8 of DESIGN.md).
+// Wavelet coherence (K7, K8, K12-K14 of DESIGN.md).
 //
 // Replaces the numerics of pycwt.wct(..., sig=False) as called from src/wct.py:106-118
 // (SURVEY Appendix A.4):
@@ -9,13 +9,19 @@
 // row zero-padded to N, then a [0.5, 1, .., 1, 0.5]/(K-1) boxcar over K scale rows
 // (scipy convolve2d 'same': rows i - K/2 .. i + (K-1)/2, zero outside).
 //
+// Launch order: wct_spectra (both series' forward FFTs), wct_plan_kernel (per-row regimes,
+// which rows take which route), wct_phase_a (rows not decimated), wct_dec_kernel (decimated
+// spectra, one launch per M) + wct_phase_a<DEC> (decimated rows), wct_phase_c (coherence of
+// band windows from band spectra), wct_phase_b (coherence of the other windows).
 // Phase A (one workgroup = one pair x a chunk of scales): per scale row two inverse
 // FFTs give W1, W2; |W1|^2 + i|W2|^2 and W12 are forward-transformed, multiplied by
 // F/(N s) (F is real and even, so the two real fields share one complex FFT) and
-// inverse-transformed: 6 in-LDS FFTs per row, the time-smoothed row
-// T = (T1, T2, Re T12, Im T12) goes to a float4 workspace.
-// Phase B (one thread = one time column of one pair): streams the S rows of T once,
-// keeps the last K rows in registers and writes WCT.
+// inverse-transformed: up to 6 in-LDS FFTs per row; a time-path row's smoothed fields
+// T = (T1, T2, Re T12, Im T12) go to the workspace.  Decimated rows (full rows whose W1,
+// W2 live in bins [0, M/2), M < N) get their forward transforms on every (N/M)-th sample
+// (wct_dec_kernel) and band inverses of M bins here.
+// Phase B (one thread = one time column of one pair): streams the time-path rows of T
+// once, keeps the last K rows in registers and writes WCT.
 #include "cwt_common.hpp"
 #include "long_path.hpp"
 
