@@ -320,7 +320,7 @@ class C4(Workload):
     name, axis, seed = "c4", "pair", 1004
     B, n, dj = 512, 8192, 1 / 8
     kernel = ("moments<float> x2 + wct_spectra<13> + wct_plan<13> + wct_phase_a<13,full-band rows> (side stream) || "
-              "wct_dec_kernel<13,5..12> + wct_phase_d<13> + wct_phase_a<13,decimated rows> + wct_phase_c<13>; "
+              "wct_dec_kernel<13,5..12> + wct_phase_a<13,decimated rows> + wct_phase_c<13>; "
               "wct_phase_b<10>")
 
     def setup(self):

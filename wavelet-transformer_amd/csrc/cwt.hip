@@ -146,7 +146,7 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
   float4* twl = prm_tab + G::MAXCHUNK;
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
-  const int t = tid - g * P::NT;
+  const int t = fft_thread<LOGN>(tid - g * P::NT);
   const long long blk = blockIdx.x;
   const long long b = blk / a.nchunks;
   const int ch = static_cast<int>(blk - b * a.nchunks);

@@ -215,7 +215,35 @@ struct FftPlan {
   static constexpr int TWL_E = P16 >= 3 ? 16 + 256 : (P16 == 2 ? 16 : 0);
   static constexpr int TWL_FLOAT4 = 2 * TWL_E;
   static constexpr int NTW_REG = NTW_REM > 0 ? NTW_REM : 1;  // registers left with TWL
+  // N = 8192 (NT = 512, eight waves): the trailing radix-2 pass pairs threads t and t + 256.
+  // Rows of this length number their threads so that those partners are lanes p and p + 32 of
+  // one wave (fft_thread); the exchange before the tail is then one v_permlane32_swap per
+  // dword instead of an LDS write + read and two barriers.
+  static constexpr bool XL = LOGN == 13;
 };
+
+// Logical thread index t (the element positions t + m NT it owns) of row thread rt: the
+// identity, except for XL rows: wave w's lanes 0-31 are t = 32 w .. 32 w + 31 and lanes 32-63
+// t + 256 (each 32-lane half still holds consecutive t: coalesced rows, conflict-free LDS).
+template <int LOGN>
+__device__ __forceinline__ int fft_thread(int rt) {
+  if constexpr (FftPlan<LOGN>::XL)
+    return 32 * (rt >> 6) + (rt & 31) + 256 * ((rt >> 5) & 1);
+  else
+    return rt;
+}
+
+// XL tail exchange: after the last radix-16 pass thread t holds outputs r at positions
+// (t / 256) 4096 + t mod 256 + 256 r; the radix-2 tail of thread t needs positions
+// t + 512 q and t + 512 q + 4096.  With X = v[2q], Y = v[2q+1], swapping the upper half of X
+// with the lower half of Y leaves (X, Y) = (x[t + 512 q], x[t + 512 q + 4096]) in every lane.
+__device__ __forceinline__ void xl_swap(cpx& x, cpx& y) {
+  float xr = x.x, xi = x.y, yr = y.x, yi = y.y;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(xr), "+v"(yr));
+  asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(xi), "+v"(yi));
+  x = mkc(xr, xi);
+  y = mkc(yr, yi);
+}
 
 // Offset of pass p's entries in the LDS twiddle table.
 __host__ __device__ constexpr int twl_base(int p) { return p <= 1 ? 0 : 16; }
@@ -435,7 +463,7 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
           apply_tw16<DIR>(v, tw + 4 * (p - 1));
         dft16<DIR>(v);
       }
-      if (!last) {
+      if (!last && !(P::XL && NBUF == 1 && p == P::P16 - 1)) {  // (XL: the tail swaps in registers)
         cpx* wbuf = lds + (NBUF == 2 ? par * bufstride : 0);
         const int idxD = (t / ns) * ns * 16 + (t & (ns - 1));
         if constexpr (NBUF == 1) __syncthreads();
@@ -453,18 +481,24 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
       constexpr int R = P::REM > 1 ? P::REM : 16;
       constexpr int Q = 16 / R;
       constexpr int tb = TWL ? 0 : 4 * (P::P16 - 1);
+      if constexpr (P::XL && NBUF == 1) {
+        static_assert(R == 2, "XL rows end with a radix-2 pass");
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
+        for (int q = 0; q < Q; ++q) xl_swap(v[2 * q], v[2 * q + 1]);
+      } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if constexpr (kAligned) {
-            const int off = q * P::NT + r * (P::N / R);
-            v[q * R + r] = rbuf[pt + off + (off >> 5)];
-          } else {
-            v[q * R + r] = rbuf[lpad(t + q * P::NT + r * (P::N / R))];
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            if constexpr (kAligned) {
+              const int off = q * P::NT + r * (P::N / R);
+              v[q * R + r] = rbuf[pt + off + (off >> 5)];
+            } else {
+              v[q * R + r] = rbuf[lpad(t + q * P::NT + r * (P::N / R))];
+            }
           }
-        }
-      if constexpr (NBUF == 2) par ^= 1;
+        if constexpr (NBUF == 2) par ^= 1;
+      }
       cpx tbase[P::NTW_REM > 0 ? P::NTW_REM : 1];
 #pragma unroll
       for (int e = 0; e < P::NTW_REM; ++e) tbase[e] = opaque(tw[tb + e]);

@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(LongRow<LOG2>::BLOCK) long_row_kernel(LongArgs
   float4* twl = lds4 + (R::ROWS * P::PADN) / 2;
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
-  const int t = tid - g * P::NT;
+  const int t = fft_thread<LOG2>(tid - g * P::NT);
   const int log1 = a.logn - LOG2;
   const int N1 = 1 << log1;
   const long long N = 1ll << a.logn;

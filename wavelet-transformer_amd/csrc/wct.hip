@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, c
   __shared__ cpx lds[G::ROWS * P::PADN];
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
-  const int t = tid - g * P::NT;
+  const int t = fft_thread<LOGN>(tid - g * P::NT);
   // row group g handles series (pair, which) = blockIdx.x * ROWS + g
   const long long item = static_cast<long long>(blockIdx.x) * G::ROWS + g;
   const bool valid = item < 2 * a.batch;
@@ -629,7 +629,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   int* q_tab = reinterpret_cast<int*>(twl + G::TWL_F4);  // row regimes (wct_regime)
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
-  const int t = tid - g * P::NT;
+  const int t = fft_thread<LOGN>(tid - g * P::NT);
   // the scale chunks of one pair share its two spectra: keep them on one XCD's L2
   const long long blk = xcd_remap(blockIdx.x, gridDim.x);
   const long long b = blk / a.nchunks;
@@ -1048,7 +1048,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   float4* twl = lds4 + (G::ROWS * P::PADN) / 2;
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
-  const int t = tid - g * P::NT;
+  const int t = fft_thread<LOGN>(tid - g * P::NT);
   const long long blk = xcd_remap(blockIdx.x, gridDim.x);
   const long long b = blk / a.nchunks;
   const int ch = static_cast<int>(blk - b * a.nchunks);
