@@ -288,7 +288,7 @@ class C3(Workload):
     """MODWT db4 J=10: 8192 x 16384, decompose + reconstruct."""
     name, axis, seed = "c3", "series", 1003
     B, n, J = 8192, 16384, 10
-    kernel = "modwt_vec_kernel<8,8,512,16>+imodwt_vec_kernel<8,8,512,3>"
+    kernel = "modwt_vec_kernel<8,8,512,16>+imodwt_hyb_kernel<8,8,512,2,4>"
 
     def setup(self):
         from wtmi.wavelets import Wavelet
@@ -299,7 +299,7 @@ class C3(Workload):
         self.x = self.torch.tensor(x, device=self.dev)
         self.units = self.local * (self.J + 1) * self.n
         self.bytes = self.local * self.n * 96  # 4 x + 44 W write + 44 W read + 4 x^
-        self.per_step = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_vec_kernel<": 1}
+        self.per_step = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_hyb_kernel<": 1}
         self.bytes_note = "96 B per series-sample (x, W write, W read, x^)"
 
     def step(self):

@@ -200,16 +200,21 @@ def test_wavedec_batched_vs_oracle():
         assert np.abs(ct[b] - ref).max() <= TOL * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("n,J", [(16384, 10), (8192, 12), (4096, 3)])
-def test_imodwt_adjoint_and_masks_at_bench_shape(n, J, db4):
+@pytest.mark.parametrize("syn", [1, 0])
+@pytest.mark.parametrize("n,J", [(16384, 10), (16384, 15), (8192, 12), (4096, 3)])
+def test_imodwt_adjoint_and_masks_at_bench_shape(n, J, syn, db4):
     """Synthesis on NON-range input (adjoint, every tap exercised) and with row masks at
-    the C3 shape (the dilation-chain kernel's levels j >= 3) vs the textbook oracle."""
+    the C3 shape vs the textbook oracle, for both n = 16384 kernels (option modwt_syn: 1 the
+    hybrid with LDS-staged low levels, 0 dilation chains only).  J = 15 reaches dilations
+    past the chain range (2^12 samples) and 2^14 = 0 mod n."""
+    from wtmi import _lib
     rng = np.random.default_rng(n + J)
     w = rng.standard_normal((2, J + 1, n)).astype(np.float32)
     ops = _ops()
     wd = torch.tensor(w, device="cuda")
-    for keep in ((1 << (J + 1)) - 1, 0b101 << (J - 2), 1 << J):
-        got = ops.imodwt(wd, db4["dec_lo"], db4["dec_hi"], keep).cpu().numpy()
+    for keep in ((1 << (J + 1)) - 1, 0b101 << (J - 2), 1 << J, 0b1011):
+        with _lib.option("modwt_syn", syn):
+            got = ops.imodwt(wd, db4["dec_lo"], db4["dec_hi"], keep).cpu().numpy()
         for b in range(2):
             wm = w[b].astype(np.float64) * np.array([(keep >> r) & 1 for r in range(J + 1)])[:, None]
             ref = ms.imodwt_direct(wm, db4["dec_lo"], db4["dec_hi"])

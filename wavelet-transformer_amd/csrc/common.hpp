@@ -108,6 +108,7 @@ struct Options {
   int wct_target_wg = 0;    // WTMI_WCT_TARGET_WG: 0 = as many as wct_min_rows allows
   int wct_min_rows = 4;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least
   int wct_dec_rows = 4;     // WTMI_WCT_DEC_ROWS: decimated scale rows per phase A workgroup
+  int modwt_syn = 1;        // WTMI_MODWT_SYN: 1 hybrid synthesis (low levels via LDS), 0 MODE 3 only
 };
 const Options& options();
 

@@ -12,6 +12,8 @@
 // One workgroup per series; the whole series stays in LDS across all J levels
 // (ping-pong through registers: read taps -> barrier -> write level j).  Rows of W
 // are written once with coalesced 16-byte stores; x is read once.
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace wtmi {
@@ -280,9 +282,14 @@ __device__ __forceinline__ void pin4(float4& v) {
   asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
 
+// acc += c s as two packed v_pk_fma_f32 (the compiler left 83 % of these as scalar v_fmac_f32:
+// twice the VALU issue of the synthesis' tap loops)
+using f2v = float __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void fma4(float4& acc, float c, const float4& s) {
-  acc.x = fmaf(c, s.x, acc.x); acc.y = fmaf(c, s.y, acc.y);
-  acc.z = fmaf(c, s.z, acc.z); acc.w = fmaf(c, s.w, acc.w);
+  const f2v cc = {c, c};
+  const f2v lo = __builtin_elementwise_fma(cc, f2v{s.x, s.y}, f2v{acc.x, acc.y});
+  const f2v hi = __builtin_elementwise_fma(cc, f2v{s.z, s.w}, f2v{acc.z, acc.w});
+  acc = make_float4(lo.x, lo.y, hi.x, hi.y);
 }
 
 // Analysis: V_{j-1} in LDS (n floats), each thread owns GROUPS float4 groups (stride T).
@@ -304,7 +311,16 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
   const int ng = n >> 2;
   const float4* xin = reinterpret_cast<const float4*>(x + b * ld);
   float* wout = w + b * static_cast<long long>(level + 1) * n;
-  for (int q = tid; q < ng; q += T) V4[q] = xin[q];
+  {
+    float4 xv[GROUPS];  // every load in flight before the first LDS write
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) xv[k] = xin[min(tid + k * T, ng - 1)];
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) {
+      pin4(xv[k]);  // not sunk into the guarded store (that re-serialises the loads)
+      if (tid + k * T < ng) V4[tid + k * T] = xv[k];
+    }
+  }
   __syncthreads();
   for (int j = 1; j <= level; ++j) {
     const int dm = dilation_mod(j, n);
@@ -511,8 +527,19 @@ __global__ void __launch_bounds__(T, 1)
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool keepV = (keep >> level) & 1ull;
   {
+    // all GROUPS loads in flight before the first LDS write (a runtime-trip loop waited on
+    // each load in turn: 8 serialised HBM round trips per workgroup)
     const float4* vr = reinterpret_cast<const float4*>(win + static_cast<long long>(level) * n);
-    for (int q = tid; q < ng; q += T) V4[vp(q)] = keepV ? vr[q] : z4;
+    float4 vin[GROUPS];
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) vin[k] = vr[min(tid + k * T, ng - 1)];
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) {
+      const float4 v = vin[k];
+      const float4 s = make_float4(keepV ? v.x : 0.f, keepV ? v.y : 0.f, keepV ? v.z : 0.f,
+                                   keepV ? v.w : 0.f);
+      if (tid + k * T < ng) V4[vp(tid + k * T)] = s;
+    }
   }
   // chain level of dilation dm (log2 of dq in groups), or -1
   auto chain_log = [&](int dm) {
@@ -557,6 +584,163 @@ __global__ void __launch_bounds__(T, 1)
   __syncthreads();
   float4* xo = reinterpret_cast<float4*>(x + b * ld_out);
   for (int q = tid; q < ng; q += T) xo[q] = V4[vp(q)];
+}
+
+// ---------------------------------------------------------------------------------
+// Synthesis, hybrid (n = 4 * GROUPS * T, a power of two; V padded in LDS, two workgroups
+// per CU).  Levels with a dilation of dq >= 2 whole groups run MODE 3's dilation chains
+// (V taps from LDS, W_j taps straight from L2).  The low levels (dm = 1, 2 samples and
+// dq = 1 group) stage W_j through LDS instead: their global tap reads were 8 dependent
+// round trips per level (one per owned group) or, along chains, 64 cache lines per load.
+//   V phase: acc = sum_l g_l V_j[. + dm l]   (LDS; W_j's coalesced loads in flight)
+//   barrier, W_j -> LDS over V_j, barrier, W phase: acc += sum_l h_l W_j[. + dm l]
+//   barrier, acc -> LDS as V_{j-1}
+// Rows whose keep bit is clear are not applied (low levels still fetch a row: a predicated
+// load is a branch, and the stack arrays that came with it cost more than the bytes).
+template <int L, int H, int NG, bool FIRST>
+__device__ __forceinline__ void chain_pass(const float4* __restrict__ S4, int q0, int dq, int base,
+                                           const float* __restrict__ c, float4* acc) {
+  float4 t[H + L - 1];
+#pragma unroll
+  for (int k = 0; k < H + L - 1; ++k) t[k] = S4[vpad((q0 + (base + k) * dq) & (NG - 1))];
+#pragma unroll
+  for (int m = 0; m < H; ++m) {
+    float4 a = FIRST ? make_float4(0.f, 0.f, 0.f, 0.f) : acc[m];
+#pragma unroll
+    for (int l = 0; l < L; ++l) fma4(a, c[l], t[m + l]);
+    acc[m] = a;
+  }
+}
+
+template <int L, int DM>
+__device__ __forceinline__ float4 window_acc(const float4* __restrict__ S4, int q, int ngm,
+                                             const float* __restrict__ c, float4 acc) {
+  constexpr int NB = ((L - 1) * DM + 3) / 4 + 1;
+  float f[4 * NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const float4 v = S4[vpad((q + u) & ngm)];
+    f[4 * u] = v.x; f[4 * u + 1] = v.y; f[4 * u + 2] = v.z; f[4 * u + 3] = v.w;
+  }
+  float r[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = fmaf(c[l], f[i + DM * l], r[i]);
+  return make_float4(r[0], r[1], r[2], r[3]);
+}
+
+using v4f = float __attribute__((ext_vector_type(4)));
+
+template <int L, int GROUPS, int T, int H, int CG>
+__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 256)))
+    imodwt_hyb_kernel(const float* __restrict__ w, int n, int level, FilterBank fb, unsigned long long keep,
+                      float* __restrict__ x, long long ld_out) {
+  constexpr int NG = GROUPS * T;
+  static_assert((NG & (NG - 1)) == 0 && GROUPS % H == 0, "power-of-two rows, H | GROUPS");
+  extern __shared__ __attribute__((aligned(16))) float4 sm4[];
+  float4* S4 = sm4;
+  const int tid = threadIdx.x;
+  const long long b = blockIdx.x;
+  const float* win = w + b * static_cast<long long>(level + 1) * n;
+  auto row4 = [&](int r) { return reinterpret_cast<const float4*>(win + static_cast<long long>(r) * n); };
+  auto kept = [&](int r) { return ((keep >> r) & 1ull) != 0; };
+  {
+    const float4* vr = row4(level);
+    float4 vin[GROUPS];
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) vin[k] = vr[tid + k * T];
+    const bool keepV = kept(level);
+#pragma unroll
+    for (int k = 0; k < GROUPS; ++k) {
+      const float4 v = vin[k];
+      S4[vpad(tid + k * T)] = make_float4(keepV ? v.x : 0.f, keepV ? v.y : 0.f, keepV ? v.z : 0.f,
+                                          keepV ? v.w : 0.f);
+    }
+  }
+  for (int j = level; j >= 1; --j) {
+    const bool useW = kept(j - 1);
+    const float4* wr = row4(j - 1);
+    const int dm = dilation_mod(j, n);
+    int tl = tid;
+    asm volatile("" : "+v"(tl));  // per-level copy: keeps address math out of LICM
+    const int dq = dm >> 2;
+    const bool chain = (dm & 3) == 0 && dq >= 1 && (dq & (dq - 1)) == 0 && NG % (GROUPS * dq) == 0;
+    const int dqlog = chain ? __builtin_ctz(dq) : 0;
+    float4 acc[GROUPS];
+    __syncthreads();  // S4 = V_j
+    if (chain && dq >= CG) {
+      float hs[L];
+      const float wsel = useW ? 1.f : 0.f;
+#pragma unroll
+      for (int l = 0; l < L; ++l) hs[l] = wsel * fb.h[l];
+      const int q0 = syn_level_chain<L, GROUPS, NG, true>(S4, wr, dqlog, hs, fb, tl, acc);
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) S4[vpad(q0 + (k << dqlog))] = acc[k];
+      continue;
+    }
+    v4f wreg[GROUPS];  // native vectors: float4 copies of loads became stack arrays
+    {
+      const v4f* wv = reinterpret_cast<const v4f*>(useW ? wr : row4(level));
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) wreg[k] = wv[tid + k * T];
+    }
+    const int q0 = chain ? chain_q0<GROUPS>(tl, dqlog) : 0;
+    auto phase = [&](const float* c, bool first) {
+      if (chain) {
+#pragma unroll
+        for (int h = 0; h < GROUPS; h += H) {
+          if (first)
+            chain_pass<L, H, NG, true>(S4, q0, dq, h, c, acc + h);
+          else
+            chain_pass<L, H, NG, false>(S4, q0, dq, h, c, acc + h);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < GROUPS; ++k) {
+          int q = tl + k * T;
+          asm volatile("" : "+v"(q));
+          const float4 a0 = first ? make_float4(0.f, 0.f, 0.f, 0.f) : acc[k];
+          if (dm == 1) {
+            acc[k] = window_acc<L, 1>(S4, q, NG - 1, c, a0);
+          } else if (dm == 2) {
+            acc[k] = window_acc<L, 2>(S4, q, NG - 1, c, a0);
+          } else {  // whole groups beyond the chain range (dq > T) or dm = 0 (2^(j-1) = 0 mod n)
+            float4 a = a0;
+#pragma unroll
+            for (int l = 0; l < L; ++l) fma4(a, c[l], S4[vpad((q + dq * l) & (NG - 1))]);
+            acc[k] = a;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) pin4(acc[k]);
+    };
+    phase(fb.g, true);
+    if (useW) {
+      __syncthreads();  // V_j reads done
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) S4[vpad(tid + k * T)] = make_float4(wreg[k].x, wreg[k].y, wreg[k].z, wreg[k].w);
+      __syncthreads();  // S4 = W_j
+      phase(fb.h, false);
+    }
+    __syncthreads();  // reads done
+    if (chain) {
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) S4[vpad(q0 + (k << dqlog))] = acc[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) S4[vpad(tl + k * T)] = acc[k];
+    }
+  }
+  __syncthreads();
+  float4* xo = reinterpret_cast<float4*>(x + b * ld_out);
+  float4 o[GROUPS];
+#pragma unroll
+  for (int k = 0; k < GROUPS; ++k) o[k] = S4[vpad(tid + k * T)];
+#pragma unroll
+  for (int k = 0; k < GROUPS; ++k) xo[tid + k * T] = o[k];
 }
 
 // ---------------------------------------------------------------------------------
@@ -772,6 +956,9 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
       launch(imodwt_vec_kernel<8, 1, 512, 0>, 512);
     else if (ng <= 1024)
       launch(imodwt_vec_kernel<8, 1, 1024, 0>, 1024);
+    else if (ng == 4096 && options().modwt_syn == 1)  // C3 A/B on one box, two orders: 1.24 ms vs
+      // 1.41-1.52 (MODE 3); global chains from dq >= 2: 1.27-1.43, from dq >= 8 1.21-1.32
+      launch_lds(imodwt_hyb_kernel<8, 8, 512, 2, 4>, 512, lds_pad);
     else if (ng <= 2048)
       launch_lds(imodwt_vec_kernel<8, 2, 1024, 3>, 1024, lds_pad);
     else

@@ -19,6 +19,7 @@ constexpr Entry kEntries[] = {
     {"wct_target_wg", &Options::wct_target_wg, 0, 1 << 24},
     {"wct_min_rows", &Options::wct_min_rows, 1, 1 << 10},
     {"wct_dec_rows", &Options::wct_dec_rows, 1, 128},
+    {"modwt_syn", &Options::modwt_syn, 0, 1},
 };
 
 Options& mutable_options() {
@@ -45,7 +46,7 @@ const Options& options() { return mutable_options(); }
 }  // namespace wtmi
 
 // Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
-// wct_min_rows, wct_dec_rows).  0 on success, -1 unknown name or out of range.  Applies to launches
+// wct_min_rows, wct_dec_rows, modwt_syn).  0 on success, -1 unknown name or out of range.  Applies to launches
 // issued after the call; not to be called while another thread is launching.
 extern "C" int wtmi_set_option(const char* name, long long value) {
   if (!name) return wtmi::kErrArg;
