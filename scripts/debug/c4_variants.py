@@ -22,10 +22,11 @@ def run(**kw):
     return ops.wct_morlet(x1, x2, sj, dt, 6.0, boxcar=K, want_uv=False, workspace=ws, **kw)
 
 
-variants = [("pow+phase", dict(want_power=True, want_phase=True), {}),
-            ("coh only", dict(), {}),
-            ("pow+phase dec_rows 8", dict(want_power=True, want_phase=True), {"wct_dec_rows": 8}),
-            ("pow+phase prune 1", dict(want_power=True, want_phase=True), {"wct_prune": 1})]
+PP = dict(want_power=True, want_phase=True)
+variants = [("pow+phase", PP, {}),
+            ("coh only", dict(), {})]
+variants += [(f"pow+phase dec_rows {r}", PP, {"wct_dec_rows": r}) for r in (2, 8, 16)]
+variants += [(f"pow+phase min_rows {r}", PP, {"wct_min_rows": r}) for r in (2, 8)]
 for rep in range(2):
     for name, kw, opts in variants:
         ctx = [_lib.option(k, v) for k, v in opts.items()]

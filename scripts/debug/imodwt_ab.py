@@ -11,8 +11,10 @@ lo = np.array([-0.010597401784997278, 0.032883011666982945, 0.030841381835986965
                -0.18703481171888114, -0.02798376941698385, 0.6308807679295904,
                0.7148465705525415, 0.23037781330885523])
 hi = np.array([(-1) ** (k + 1) * lo[7 - k] for k in range(8)])
-B, n = 8192, 16384
-variants = [int(a) for a in (sys.argv[1:] or ["0", "1", "2", "3"])]
+import os
+n = int(os.environ.get("N", 16384))
+B = 8192 * 16384 // n
+variants = [int(a) for a in (sys.argv[1:] or ["0", "1"])]
 
 
 def timed(fn, reps=20):

@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(T, 1)
 }
 
 // ---------------------------------------------------------------------------------
-// Synthesis, hybrid (n = 4 * GROUPS * T, a power of two; V padded in LDS, two workgroups
+// Synthesis, hybrid (n = 4 * GROUPS * T = 8192 or 16384; V padded in LDS, two workgroups
 // per CU).  Levels with a dilation of dq >= 2 whole groups run MODE 3's dilation chains
 // (V taps from LDS, W_j taps straight from L2).  The low levels (dm = 1, 2 samples and
 // dq = 1 group) stage W_j through LDS instead: their global tap reads were 8 dependent
@@ -959,6 +959,8 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
     else if (ng == 4096 && options().modwt_syn == 1)  // C3 A/B on one box, two orders: 1.24 ms vs
       // 1.41-1.52 (MODE 3); global chains from dq >= 2: 1.27-1.43, from dq >= 8 1.21-1.32
       launch_lds(imodwt_hyb_kernel<8, 8, 512, 2, 4>, 512, lds_pad);
+    else if (ng == 2048 && options().modwt_syn == 1)
+      launch_lds(imodwt_hyb_kernel<8, 4, 512, 2, 4>, 512, lds_pad);
     else if (ng <= 2048)
       launch_lds(imodwt_vec_kernel<8, 2, 1024, 3>, 1024, lds_pad);
     else
