@@ -253,10 +253,12 @@ __device__ __forceinline__ int lpad(int i) { return i + (i >> 5); }
 // exp(+2 pi i num / den) for a power-of-two den <= 2^14: 2 num / den is exact in
 // float, and sincospif is accurate to ~1 ulp -- the double-precision form cost a
 // measurable share of each workgroup's start-up (8-16 fp64 sincospi per thread).
+// The quotient is a power-of-two scaling (ldexp): exact, and no IEEE division sequence
+// where den is not a compile-time constant (the LDS twiddle-table fill).
 __device__ __forceinline__ cpx expi_frac(int num, int den) {
   num &= den - 1;
   float s, c;
-  sincospif(2.f * static_cast<float>(num) / static_cast<float>(den), &s, &c);
+  sincospif(ldexpf(static_cast<float>(num), 1 - __builtin_ctz(den)), &s, &c);
   return mkc(c, s);
 }
 
