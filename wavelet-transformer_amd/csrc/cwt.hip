@@ -304,7 +304,13 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   // Few, long workgroups: each one's start-up (twiddles, forward FFT) amortises over
   // more scales.  Measured (ms): C2 (LOGN 12, 3 WG/CU) 1024 WG 0.871, 2048 0.839,
   // 4096 0.860; C5 chunk (LOGN 13, 2 WG/CU) 512 30.9, 1024 30.86, 2048 31.2, 4096 32.9.
-  const int target = options().cwt_target_wg > 0 ? options().cwt_target_wg : (LOGN >= 13 ? 1024 : 2048);
+  // Small batches (a strong-scaling shard) get fewer, longer workgroups: 2 per series, at
+  // least 512.  C2 shapes on one box (ms, target 2048 -> this rule): 128 series 0.128 -> 0.115,
+  // 512 series 0.411 -> 0.402, 256 a tie, 1024 unchanged (2048 either way).
+  const long long by_batch = 2 * a.batch < 512 ? 512 : 2 * a.batch;
+  const int cap = LOGN >= 13 ? 1024 : 2048;
+  const int target = options().cwt_target_wg > 0 ? options().cwt_target_wg
+                                                 : static_cast<int>(by_batch < cap ? by_batch : cap);
   long long want = (target + a.batch - 1) / a.batch;
   const int max_chunks = (a.S + 4 * rows - 1) / (4 * rows);
   int nch = static_cast<int>(want < 1 ? 1 : want);
