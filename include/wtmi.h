@@ -150,10 +150,12 @@ int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batc
  * Launch-policy knobs, read from WTMI_<NAME> environment variables once at first use
  * and settable here: cwt_prune (2 band rows + narrowed entry passes, 1 band rows, 0 full
  * transforms), cwt_target_wg, wct_prune (2 band rows + decimated spectra of full rows, 1 band
- * rows, 0 full transforms), wct_target_wg, wct_min_rows, wct_dec_rows (decimated scale rows per
- * WCT phase-A workgroup), modwt_syn (n = 8192 / 16384 synthesis: 1 hybrid kernel with the low levels
- * staged through LDS, 0 dilation chains only).  The prune and kernel switches exist so that
- * tests can compare the paths; results agree to fp32 resolution either way.  Not thread-safe against concurrent launches.
+ * rows, 0 full transforms), wct_target_wg, wct_min_rows and wct_dec_rows (scale rows per WCT
+ * workgroup and decimated rows per phase-A workgroup; 0 = chosen by batch size), modwt_syn
+ * (n = 8192 / 16384 synthesis: 1 hybrid kernel with the low levels staged through LDS, 0
+ * dilation chains only).  The prune and kernel switches exist so that tests can compare the
+ * paths; results agree to fp32 resolution either way.  Not thread-safe against concurrent
+ * launches.
  * wtmi_set_option: 0, or -1 for an unknown name / out-of-range value;
  * wtmi_get_option: the value, or -1 for an unknown name.                             */
 int wtmi_set_option(const char* name, long long value);

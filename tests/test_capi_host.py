@@ -137,7 +137,7 @@ def test_launch_options_set_get_and_reject():
         assert _lib.get_option("cwt_prune") == 0
         with _lib.option("wct_min_rows", 7):
             assert _lib.get_option("wct_min_rows") == 7
-    assert _lib.get_option("wct_min_rows") == 4
+    assert _lib.get_option("wct_min_rows") == 0  # 0 = by batch (wct.hip wct_min_rows)
     lib = _lib.load()
     assert lib.wtmi_set_option(b"cwt_prune", 3) == -1  # out of range
     assert lib.wtmi_set_option(b"no_such_option", 1) == -1

@@ -106,8 +106,8 @@ struct Options {
   int cwt_target_wg = 0;    // WTMI_CWT_TARGET_WG: workgroups per CWT launch, 0 = by size
   int wct_prune = 2;        // WTMI_WCT_PRUNE: 2 band rows + decimated spectra, 1 band rows, 0 full
   int wct_target_wg = 0;    // WTMI_WCT_TARGET_WG: 0 = as many as wct_min_rows allows
-  int wct_min_rows = 4;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least
-  int wct_dec_rows = 4;     // WTMI_WCT_DEC_ROWS: decimated scale rows per phase A workgroup
+  int wct_min_rows = 0;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least (0 = by batch)
+  int wct_dec_rows = 0;     // WTMI_WCT_DEC_ROWS: decimated scale rows per phase A workgroup (0 = by batch)
   int modwt_syn = 1;        // WTMI_MODWT_SYN: 1 hybrid synthesis (low levels via LDS), 0 MODE 3 only
 };
 const Options& options();

@@ -17,8 +17,8 @@ constexpr Entry kEntries[] = {
     {"cwt_target_wg", &Options::cwt_target_wg, 0, 1 << 24},
     {"wct_prune", &Options::wct_prune, 0, 2},
     {"wct_target_wg", &Options::wct_target_wg, 0, 1 << 24},
-    {"wct_min_rows", &Options::wct_min_rows, 1, 1 << 10},
-    {"wct_dec_rows", &Options::wct_dec_rows, 1, 128},
+    {"wct_min_rows", &Options::wct_min_rows, 0, 1 << 10},
+    {"wct_dec_rows", &Options::wct_dec_rows, 0, 128},
     {"modwt_syn", &Options::modwt_syn, 0, 1},
 };
 

@@ -1089,6 +1089,19 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   }
 }
 
+// Rows per workgroup when the options leave them at 0 (auto): shorter workgroups for small
+// batches (one GPU's share of a strong-scaling run), so the grids still fill the CUs.  C4 rows
+// at 64 / 128 / 256 / 512 pairs, one box (ms, 4+4 rows -> this rule): 0.675 -> 0.600,
+// 1.075 -> 1.023, 1.914 -> 1.894, 3.54 unchanged.
+static int wct_min_rows(long long batch) {
+  const int o = options().wct_min_rows;
+  return o > 0 ? o : (batch <= 128 ? 1 : batch <= 256 ? 2 : 4);
+}
+static int wct_dec_rows_per_wg(long long batch) {
+  const int o = options().wct_dec_rows;
+  return o > 0 ? o : (batch <= 256 ? 2 : 4);
+}
+
 template <int LOGN>
 static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY, int* plan, int K,
                           float* coh, hipStream_t st) {
@@ -1109,7 +1122,7 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   // 3.95-4.09 vs 3 rows 4.01-4.09, 2 rows 4.03-4.13.  Default: 4-row workgroups.
   const long long target = options().wct_target_wg > 0 ? options().wct_target_wg : (1ll << 30);
   long long want = (target + a.batch - 1) / a.batch;
-  const int min_rows = options().wct_min_rows;  // rows per workgroup, at least
+  const int min_rows = wct_min_rows(a.batch);  // rows per workgroup, at least
   const int max_chunks = (a.S + min_rows * rows - 1) / (min_rows * rows);
   int nch = static_cast<int>(want < 1 ? 1 : want);
   if (nch > max_chunks) nch = max_chunks < 1 ? 1 : max_chunks;
@@ -1151,7 +1164,7 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
       }
       // decimated rows cost one to three band inverses each: chunks of their own length
       CwtArgs ad = a;
-      ad.chunk = ((options().wct_dec_rows + rows - 1) / rows) * rows;
+      ad.chunk = ((wct_dec_rows_per_wg(a.batch) + rows - 1) / rows) * rows;
       if (ad.chunk > G::MAXCHUNK) ad.chunk = G::MAXCHUNK;
       ad.nchunks = (a.S + ad.chunk - 1) / ad.chunk;
       hipLaunchKernelGGL((wct_phase_a<LOGN, true, true>), dim3(static_cast<unsigned>(a.batch * ad.nchunks)),
