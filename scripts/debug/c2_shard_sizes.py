@@ -25,11 +25,11 @@ def timed(x, out):
     return e0.elapsed_time(e1) / 50
 
 
-for B in (1024, 512, 256, 128):
+for B in [int(a) for a in sys.argv[1:]] or (1024, 512, 256, 128):
     x = torch.randn(B, n, device="cuda")
     out = torch.empty((B, 128, n), dtype=torch.complex64, device="cuda")
     gb = B * 128 * n * 8 / 1e9 + B * n * 4 / 1e9
-    for wg in (0, 512, 1024, 2048, 4096):
+    for wg in (0, 256, 384, 512, 768, 1024, 1536):
         with _lib.option("cwt_target_wg", wg):
             ms = timed(x, out)
         print(f"B={B:5d} target_wg={wg:5d} {ms:.4f} ms  {gb / ms:.2f} TB/s", flush=True)

@@ -32,8 +32,8 @@ if which == "c4":
         x1 = torch.randn(B, n, device="cuda").cumsum(1)
         x2 = torch.randn(B, n, device="cuda").cumsum(1)
         ws = torch.empty(ops.wct_workspace_bytes(B, n, len(sj)), dtype=torch.uint8, device="cuda")
-        for opts in ({}, {"wct_min_rows": 2, "wct_dec_rows": 2}, {"wct_min_rows": 1, "wct_dec_rows": 1},
-                     {"wct_min_rows": 1, "wct_dec_rows": 2}, {"wct_min_rows": 2, "wct_dec_rows": 1}):
+        for opts in ({}, {"wct_min_rows": 4, "wct_dec_rows": 4}, {"wct_min_rows": 2, "wct_dec_rows": 2},
+                     {"wct_min_rows": 1, "wct_dec_rows": 2}):
             ctx = [_lib.option(k, v) for k, v in opts.items()]
             for c in ctx:
                 c.__enter__()

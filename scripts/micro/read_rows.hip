@@ -46,6 +46,28 @@ __global__ void __launch_bounds__(T) read_rows(const float4* __restrict__ w, flo
   for (int k = 0; k < G; ++k) x[static_cast<long long>(blockIdx.x) * kNG + tid + k * T] = acc[k];
 }
 
+// Analysis skeleton: read one row, write 11 rows (one per "level", LDS round trip each).
+template <int T>
+__global__ void __launch_bounds__(T) write_rows(const float4* __restrict__ x, float4* __restrict__ w) {
+  constexpr int G = kNG / T;
+  __shared__ float4 s[kNG];
+  const int tid = threadIdx.x;
+  float4 v[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) v[k] = x[static_cast<long long>(blockIdx.x) * kNG + tid + k * T];
+  float4* base = w + static_cast<long long>(blockIdx.x) * kR * kNG;
+  for (int r = 0; r < kR; ++r) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) base[static_cast<long long>(r) * kNG + tid + k * T] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < G; ++k) s[tid + k * T] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < G; ++k) v[k] = s[(tid + 37 + k * T) & (kNG - 1)];
+  }
+}
+
 template <typename K>
 static float run(K kernel, int threads, const float4* w, float4* x) {
   hipEvent_t a, b;
@@ -72,6 +94,8 @@ int main() {
   const float t2 = run(read_rows<1024, 1, false>, 1024, w, x);
   const float t3 = run(read_rows<512, 1, true>, 512, w, x);
   const float t4 = run(read_rows<1024, 2, false>, 1024, w, x);
+  const float t5 = run(write_rows<512>, 512, x, w);
+  printf("analysis skeleton (1 row in, 11 out, 512 thr): %.4f ms %.2f TB/s\n", t5, gb / t5);
   printf("512 thr, 1 row in flight: %.4f ms %.2f TB/s\n", t0, gb / t0);
   printf("512 thr, 2 rows in flight: %.4f ms %.2f TB/s\n", t1, gb / t1);
   printf("1024 thr, 1 row in flight: %.4f ms %.2f TB/s\n", t2, gb / t2);
