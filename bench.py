@@ -132,6 +132,19 @@ def host_cpu_info():
     return {"usable": usable, "affinity": visible, "cgroup_quota": quota, "model": model}
 
 
+def cpu_baseline_child(args):
+    """The CPU baseline in a child process (a fresh interpreter that never touches the GPU):
+    this process then never holds a worker pool, and with --cpu-baseline-when after the host
+    cores are busy only once the GPU's timed region is over."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--cpu-baseline-only",
+           "--cpu-workers", str(args.cpu_workers), "--cpu-per-worker", str(args.cpu_per_worker)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError(f"CPU baseline child failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline(cfg, per_worker, workers, info):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -458,6 +471,10 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--cpu-per-worker", type=int, default=0, help="0 = per-config default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-when", default="after", choices=["before", "after"],
+                    help="run the CPU baseline (a child process) before GPU set-up or after the "
+                         "timed region: run before, it slowed the timed C2 kernel 5-12 %%")
+    ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo + the stub workload only (launcher tests)")
     args = ap.parse_args()
@@ -473,12 +490,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     wl_cls = CONFIGS[args.config]
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "stub":
-        # before any GPU initialisation (spawned workers never touch the GPU)
+    if args.cpu_baseline_only:  # the child of cpu_baseline_child(): no GPU, one JSON line
         info = host_cpu_info()
         workers = args.cpu_workers or info["usable"]
-        cpu = cpu_baseline(args.config, args.cpu_per_worker, workers, info)
+        print(json.dumps(cpu_baseline(args.config, args.cpu_per_worker, workers, info)), flush=True)
+        return
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "stub"
+    cpu = cpu_baseline_child(args) if want_cpu and args.cpu_baseline_when == "before" else None
 
     import torch
     import torch.distributed as dist
@@ -550,6 +568,8 @@ def main():
     else:
         tmax, units_all = elapsed, float(wl.units)
     check = wl.check() if rank == 0 and wl.local else None
+    if want_cpu and cpu is None:  # after the timed region (default)
+        cpu = cpu_baseline_child(args)
 
     if rank == 0:
         achieved = wl.bytes / (kern_ms * 1e-3) / 1e9
