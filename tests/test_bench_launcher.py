@@ -62,3 +62,15 @@ def test_shard_rows_do_not_depend_on_world_size():
     b1, b2 = bench.synth_rows(9, 0, 100, 32, pairs=True)
     np.testing.assert_array_equal(a1, b1[10:90])
     np.testing.assert_array_equal(a2, b2[10:90])
+
+
+def test_cpu_baseline_child_prints_one_record():
+    """The CPU baseline runs in a child interpreter (bench.py --cpu-baseline-only), after the
+    timed region: it must print one JSON record with the contract's keys and never import torch."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c3",
+                        "--cpu-baseline-only", "--cpu-workers", "1", "--cpu-per-worker", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["cores"] == 1 and rec["kind"] == "port" and rec["unit"] == "coeffs/s"
+    assert rec["value"] > 0 and "sample" in rec and "cpu_model" in rec
