@@ -41,16 +41,21 @@ __global__ void __launch_bounds__(kStatThreads) moments_kernel(const void* x, lo
   __shared__ double sh[kStatThreads / 64];
   const long long b = blockIdx.x;
   const long long base = b * ld;
+  // unrolled by 8: the loads of eight iterations are in flight together (the plain strided
+  // loop waited on each load in turn: 24 us for 512 series of 8192 samples, latency-bound)
   double s = 0.0;
+#pragma unroll 8
   for (int i = threadIdx.x; i < n; i += kStatThreads) s += ld_elem<T>(x, base + i);
   const double mean = block_sum(s, sh) / n;
   const double tbar = 0.5 * (n - 1);
   double sxx = 0.0, sxt = 0.0, sl1 = 0.0;
+#pragma unroll 8
   for (int i = threadIdx.x; i < n; i += kStatThreads) {
     const double d = ld_elem<T>(x, base + i) - mean;
     sxx += d * d;
     sxt += d * (i - tbar);
-    if (i + 1 < n) sl1 += d * (ld_elem<T>(x, base + i + 1) - mean);
+    const double dn = ld_elem<T>(x, base + min(i + 1, n - 1)) - mean;  // no branch around the load
+    sl1 += (i + 1 < n) ? d * dn : 0.0;
   }
   sxx = block_sum(sxx, sh);
   sxt = block_sum(sxt, sh);
