@@ -65,6 +65,7 @@ __global__ void __launch_bounds__(1024) modwt_kernel(const float* __restrict__ x
   const int taps = LT > 0 ? LT : L;
   const bool vec = (n & 3) == 0;
   const int ng = n >> 2;
+#pragma unroll 4  // several loads in flight per thread (a plain strided loop waits on each)
   for (int i = tid; i < n; i += T) V[i] = xin[i];
   __syncthreads();
   for (int j = 1; j <= level; ++j) {
@@ -159,11 +160,13 @@ __global__ void __launch_bounds__(1024) imodwt_kernel(const float* __restrict__ 
   const bool vec = (n & 3) == 0;
   const int ng = n >> 2;
   const bool keepV = (keep >> level) & 1ull;
+#pragma unroll 4
   for (int i = tid; i < n; i += T) V[i] = keepV ? win[static_cast<long long>(level) * n + i] : 0.f;
   for (int j = level; j >= 1; --j) {
     const bool useW = (keep >> (j - 1)) & 1ull;
     if (useW) {
       const float* wrow = win + static_cast<long long>(j - 1) * n;
+#pragma unroll 4
       for (int i = tid; i < n; i += T) Wj[i] = wrow[i];
     }
     __syncthreads();
