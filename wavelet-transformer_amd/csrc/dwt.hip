@@ -38,6 +38,7 @@ __global__ void __launch_bounds__(kDwtThreads) wavedec_kernel(const float* __res
   const long long b = blockIdx.x;
   const float* xin = x + b * ld;
   float* out = coeffs + b * total;
+#pragma unroll 4  // several loads in flight per thread
   for (int i = threadIdx.x; i < n; i += kDwtThreads) A[i] = xin[i];
   __syncthreads();
   // offset of cD_j (pywt list index level - j + 1) = total - sum_{i<=j} len(cD_i)
@@ -83,6 +84,7 @@ __global__ void __launch_bounds__(kDwtThreads) waverec_kernel(const float* __res
   for (int j = 1; j <= level; ++j) lens[j] = (lens[j - 1] + F - 1) / 2;
   int alen = lens[level];
   const bool keepA = keep & 1ull;
+#pragma unroll 4  // several loads in flight per thread
   for (int i = threadIdx.x; i < alen; i += kDwtThreads) A[i] = keepA ? cin[i] : 0.f;
   long long off = alen;
   for (int k = 1; k <= level; ++k) {

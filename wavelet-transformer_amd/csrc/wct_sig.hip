@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(kHistThreads) coherence_hist_kernel(
   const float fb = static_cast<float>(nbins);
   for (long long p = part; p < batch; p += parts) {
     const float* row = coh + (p * S + s) * n0;
+#pragma unroll 4  // several loads in flight per thread
     for (long long t = lo + threadIdx.x; t < hi; t += kHistThreads) {
       const float r = row[t];
       if (!(r == r)) continue;
