@@ -430,32 +430,67 @@ def pmc_traffic(cfg, per_step):
 
 
 # -------------------------------------------------------------------- launcher
-def launch_ranks(n, argv):
+def _stop_all(procs, grace=10.0):
+    """SIGTERM every live rank, then SIGKILL what is still alive after `grace` seconds."""
+    for q in procs:
+        if q.poll() is None:
+            q.terminate()
+    deadline = time.monotonic() + grace
+    for q in procs:
+        try:
+            q.wait(timeout=max(0.1, deadline - time.monotonic()))
+        except Exception:  # noqa: BLE001  (subprocess.TimeoutExpired)
+            q.kill()
+            q.wait()
+
+
+def launch_ranks(n, argv, timeout_s=0.0):
     """``python bench.py --gpus N`` without torch.distributed.run: start N fresh rank
     processes (this parent never initialises the GPU), stream their output, stop the
-    others as soon as one fails, and return the worst exit status."""
+    others as soon as one fails, and return the worst exit status.  The ranks never
+    outlive this parent: on any exit path (an exception, SIGINT / SIGTERM, or the
+    optional wall-clock limit `timeout_s`, exit status 124) the survivors are terminated
+    and then killed."""
+    import signal
     import socket
     import subprocess
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+
+    def _on_signal(signum, _frame):
+        raise SystemExit(128 + signum)
+
+    old = {sig: signal.signal(sig, _on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
-    while procs:
-        for p in list(procs):
-            code = p.poll()
-            if code is None:
-                continue
-            procs.remove(p)
-            if code != 0:
-                rc = rc or code
-                for q in procs:
-                    q.terminate()
-        time.sleep(0.05)
+    t0 = time.monotonic()
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                          env=env))
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    _stop_all(live)
+            if timeout_s and live and time.monotonic() - t0 > timeout_s:
+                print(f"bench: ranks still running after {timeout_s:.0f} s; stopping them",
+                      file=sys.stderr, flush=True)
+                rc = rc or 124
+                _stop_all(live)
+            time.sleep(0.05)
+    finally:
+        _stop_all(procs)
+        for sig, h in old.items():
+            signal.signal(sig, h)
     return rc
 
 
@@ -477,12 +512,17 @@ def main():
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo + the stub workload only (launcher tests)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, one GPU per rank: the measured mode) or gloo (smoke mode: "
+                         "ranks may share a GPU, rank r on cuda:(r mod device count))")
+    ap.add_argument("--rank-timeout", type=float, default=0.0,
+                    help="self-launched ranks: wall-clock limit in seconds (0 = none)")
     args = ap.parse_args()
     if args.device == "cpu" and args.config != "stub":
         ap.error("--device cpu runs only --config stub")
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return launch_ranks(args.gpus, sys.argv[1:])
+        return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -500,15 +540,19 @@ def main():
 
     import torch
     import torch.distributed as dist
+
+    from wtmi import sharding
+    rccl = args.device == "cuda" and args.dist_backend == "nccl"
     if args.device == "cuda":
-        dev = torch.device("cuda", local)
+        # RCCL: one GPU per rank.  gloo smoke mode: ranks may share a device.
+        dev = torch.device("cuda", local if rccl else local % torch.cuda.device_count())
         torch.cuda.set_device(dev)
         sync = torch.cuda.synchronize
     else:
         dev = torch.device("cpu")
         sync = lambda: None  # noqa: E731
     if world > 1:
-        if args.device == "cuda":
+        if rccl:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
@@ -518,8 +562,8 @@ def main():
 
     def barrier():
         if world > 1:
-            if args.device == "cuda":
-                dist.barrier(device_ids=[local])
+            if rccl:
+                dist.barrier(device_ids=[dev.index])
             else:
                 dist.barrier()
 
@@ -558,15 +602,10 @@ def main():
     else:
         kern_ms = elapsed / max(args.steps, 1) * 1e3
 
-    t = torch.tensor([elapsed, float(wl.units)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tt = t[:1].clone()
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        uu = t[1:].clone()
-        dist.all_reduce(uu, op=dist.ReduceOp.SUM)
-        tmax, units_all = float(tt.item()), float(uu.item())
-    else:
-        tmax, units_all = elapsed, float(wl.units)
+    # max over ranks of the timed region, sum of the units (a device tensor under RCCL,
+    # a host tensor under gloo: wtmi.sharding)
+    tmax = sharding.max_over_ranks(elapsed)
+    units_all = sharding.sum_over_ranks(float(wl.units))
     check = wl.check() if rank == 0 and wl.local else None
     if want_cpu and cpu is None:  # after the timed region (default)
         cpu = cpu_baseline_child(args)
@@ -576,6 +615,11 @@ def main():
         traffic, tsrc = pmc_traffic(args.config, wl.per_step)
         cfg = wl.config()
         cfg.update(wl.shard_config(world, args.scaling))
+        if world > 1:
+            cfg["dist_backend"] = "rccl" if rccl else "gloo"
+            if not rccl and args.device == "cuda":
+                cfg["devices"] = "shared: rank r on cuda:(r mod %d) (gloo smoke mode, not a scaling "\
+                                 "measurement)" % torch.cuda.device_count()
         line = {
             "metric": METRIC,
             "value": units_all * args.steps / tmax,

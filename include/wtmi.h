@@ -154,8 +154,9 @@ int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batc
  * workgroup and decimated rows per phase-A workgroup; 0 = chosen by batch size), modwt_syn
  * (n = 8192 / 16384 synthesis: 1 hybrid kernel with the low levels staged through LDS, 0
  * dilation chains only).  The prune and kernel switches exist so that tests can compare the
- * paths; results agree to fp32 resolution either way.  Not thread-safe against concurrent
- * launches.
+ * paths; results agree to fp32 resolution either way.  The environment gives the process
+ * defaults; wtmi_set_option changes the CALLING thread's value only (thread-local), so it
+ * never races a launch issued by another thread, and wtmi_get_option reads it back.
  * wtmi_set_option: 0, or -1 for an unknown name / out-of-range value;
  * wtmi_get_option: the value, or -1 for an unknown name.                             */
 int wtmi_set_option(const char* name, long long value);

@@ -228,8 +228,11 @@ def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95,
     W1, sj, freq, coi, _, _ = cwt(y1n, dt, **kw)
     W2, sj, freq, coi, _, _ = cwt(y2n, dt, **kw)
     W12 = W1 * W2.conj()
-    # std1 / std2 are the RAW series' deviations, taken before normalising and kept for the
-    # test (signif = s1 s2 sqrt(Pk1 Pk2) chi2/2, no condition on normalize)
+    # pycwt resets std1 = std2 = 1 when the series were normalised: the transformed series
+    # then have unit variance, so their red-noise spectra are scaled by 1, not by the raw
+    # variances (SURVEY A.4 step 4 omits this condition)
+    if normalize:
+        std1 = std2 = 1.0
     a1, _, _ = ar1(y1)
     a2, _, _ = ar1(y2)
     Pk1 = ar1_spectrum(freq * dt, a1)

@@ -144,3 +144,21 @@ def test_launch_options_set_get_and_reject():
     assert lib.wtmi_get_option(b"no_such_option") == -1
     with pytest.raises(_lib.WtmiError):
         _lib.get_option("no_such_option")
+
+
+def test_launch_options_are_thread_local():
+    """wtmi_set_option changes the calling thread's options only (csrc/options.hip), so
+    a test or A/B script overriding one cannot race a launch on another thread."""
+    import threading
+
+    from wtmi import _lib
+    default = _lib.get_option("cwt_prune")
+    seen = {}
+    with _lib.option("cwt_prune", 1 if default != 1 else 0):
+        mine = _lib.get_option("cwt_prune")
+        t = threading.Thread(target=lambda: seen.setdefault("other", _lib.get_option("cwt_prune")))
+        t.start()
+        t.join()
+    assert mine != default
+    assert seen["other"] == default
+    assert _lib.get_option("cwt_prune") == default

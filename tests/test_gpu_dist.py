@@ -1,0 +1,105 @@
+"""Multi-rank path with the REAL engine, on the one-GPU box.
+
+Two ranks over gloo, both on cuda:0, each run the HIP CWT and MODWT on their
+``shard_range`` block and gather host-side to rank 0 (wtmi.sharding); the gathered
+batch must be bit-identical to one process transforming the whole batch (the kernels
+compute every series independently).  The bench's multi-rank mode runs the same way in
+``--dist-backend gloo`` smoke mode: two ranks cover the global C2 batch.
+"""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B, N0, S, J = 13, 1500, 40, 6
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batch():
+    from gpu_helpers import red_batch
+    return red_batch(99, B, N0)
+
+
+def _transform(x):
+    """CWT W (complex64) and MODWT rows of a [b, n0] host batch on cuda:0."""
+    import torch
+    from wtmi import ops
+    from wtmi.wavelets import Wavelet
+    sj = 2 / 12 * 2 ** (np.arange(S) / 12)
+    xd = torch.tensor(x, device="cuda:0")
+    W = ops.cwt_morlet(xd, sj, 1 / 12)["w"]
+    w = Wavelet("db4")
+    M = ops.modwt(xd, w.dec_lo, w.dec_hi, J)
+    return W, M
+
+
+def _rank_main(rank, world, port, out_dir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "wavelet-transformer_amd"), os.path.join(ROOT, "tests")]
+    import torch
+    import torch.distributed as dist
+    from wtmi import sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    x = _batch()
+    s, e = sharding.shard_range(B, rank, world)
+    W, M = _transform(x[s:e])
+    gW = sharding.gather_to_rank0(torch.view_as_real(W), B)
+    gM = sharding.gather_to_rank0(M, B)
+    t = sharding.max_over_ranks(1.0 + rank)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "W.npy"), torch.view_as_complex(gW).numpy())
+        np.save(os.path.join(out_dir, "M.npy"), gM.numpy())
+        np.save(os.path.join(out_dir, "t.npy"), np.array([t]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_on_one_gpu_gather_bitwise(tmp_path):
+    import torch
+    port = _free_port()
+    code = ("import sys; sys.path[:0] = [%r, %r]; import test_gpu_dist as t; "
+            "t._rank_main(int(sys.argv[1]), 2, %d, %r)"
+            % (os.path.join(ROOT, "tests"), ROOT, port, str(tmp_path)))
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], cwd=ROOT) for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0]
+    W, M = _transform(_batch())
+    np.testing.assert_array_equal(np.load(tmp_path / "W.npy"), W.cpu().numpy())
+    np.testing.assert_array_equal(np.load(tmp_path / "M.npy"), M.cpu().numpy())
+    assert float(np.load(tmp_path / "t.npy")[0]) == 2.0
+    torch.cuda.synchronize()
+
+
+def test_bench_two_ranks_gloo_smoke():
+    """bench.py --gpus 2 --dist-backend gloo: both ranks on the one GPU, the global C2
+    batch covered (512 series each), one JSON line with n_gpus 2."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c2",
+           "--dist-backend", "gloo", "--steps", "3", "--warmup", "1", "--prewarm-s", "0",
+           "--rank-timeout", "240"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    cfg = line["config"]
+    assert cfg["global_batch"] == 1024 and cfg["per_rank_batch"] == 512
+    assert cfg["dist_backend"] == "gloo"
+    assert line["value"] > 0
+    assert line["check"]["rank0_first_last_series_max_row_rel_err_vs_oracle"] < 1e-5

@@ -234,6 +234,45 @@ def test_src_xwt_and_wct():
     assert fin.any() and (rs.significance_levels[fin] > 0).all()
 
 
+@pytest.mark.parametrize("normalize", [True, False])
+def test_xwt_significance_on_app_shaped_series(normalize):
+    """sigma != 1 inputs as create_xwt_dict builds them (detrended, then divided by the
+    ORIGINAL std: src/utils/transform_helpers.py:74-75, src/utils/wavelet_helpers.py:22-57).
+    pycwt.xwt resets std1 = std2 = 1 when it normalises, so the significance ratio of
+    run_xwt must not carry sigma1 sigma2 (parity unpinned: pycwt is absent, the oracle
+    restates it)."""
+    import src.xwt as xwt
+    from wtmi import transforms
+    rng = np.random.default_rng(77)
+    n = 700
+    t = np.arange(n)
+    y1r = 3.0 * red_series(rng, n) + 0.05 * t + 40
+    y2r = 0.5 * np.roll(y1r, 5) + 2.0 * red_series(rng, n) - 0.1 * t
+    y1, y2 = gs.standardize_series(y1r), gs.standardize_series(y2r)
+    assert abs(y1.std() - 1) > 0.05 and abs(y2.std() - 1) > 0.05
+    # pycwt-level xwt under both normalize values
+    W12, coi, freq, signif = transforms.xwt(y1, y2, xwt.DT, xwt.DJ, xwt.S0, normalize=normalize)
+    rW12, rcoi, rfreq, rsignif = pc.xwt(y1, y2, xwt.DT, xwt.DJ, xwt.S0, normalize=normalize)
+    np.testing.assert_allclose(signif, rsignif, rtol=1e-9)
+    assert row_relerr(W12, rW12).max() < 2e-5
+    ratio = rsignif / pc.xwt(y1, y2, xwt.DT, xwt.DJ, xwt.S0, normalize=True)[3]
+    if normalize:
+        np.testing.assert_allclose(ratio, 1.0)
+    else:
+        np.testing.assert_allclose(ratio, y1.std() * y2.std(), rtol=1e-12)
+    # drop-in run_xwt: the reference always calls pycwt.xwt with normalize=True
+    d = xwt.DataForXWT(y1, y2, xwt.MOTHER_DICT["morlet"], xwt.DT, xwt.DJ, xwt.S0, xwt.LEVELS)
+    r = xwt.run_xwt(d, normalize=normalize)
+    if normalize:
+        ref = gs.run_xwt(y1, y2, xwt.DT, xwt.DJ, xwt.S0, xwt.LEVELS)
+        assert row_relerr(r.power, ref[0]).max() < 5e-5
+        assert row_relerr(r.significance_levels, ref[2]).max() < 5e-5
+    else:  # documented deviation from the reference's NameError: raw W12 and W12 / signif
+        rW12n, _, rf, rs = pc.xwt(y1, y2, xwt.DT, xwt.DJ, xwt.S0)
+        assert row_relerr(r.power, rW12n).max() < 5e-5
+        assert row_relerr(r.significance_levels, rW12n / rs[:, None]).max() < 5e-5
+
+
 def test_src_dwt_and_modwt(dwt_golden, modwt_golden):
     import src.dwt as dwt
     import src.modwt as modwt

@@ -173,3 +173,23 @@ def test_run_cwt_glue_quirks():
     np.testing.assert_array_equal(p, p2)  # quirk B.1
     with pytest.raises(ValueError):
         gs.standardize_series(y, detrend=True, remove_mean=True)
+
+
+def test_xwt_significance_sigma_reset():
+    """pycwt.xwt: std1 = std2 = 1 when the series are normalised (the transformed series
+    have unit variance), the raw deviations otherwise.  Invariant to rescaling the inputs
+    under normalize=True; scales with sigma1 sigma2 under normalize=False."""
+    rng = np.random.default_rng(9)
+    e = rng.standard_normal((2, 300))
+    y1 = np.zeros(300)
+    for t in range(1, 300):
+        y1[t] = 0.7 * y1[t - 1] + e[0, t]
+    y2 = 0.5 * np.roll(y1, 2) + e[1]
+    s = pc.xwt(y1, y2, DT, 1 / 8, 2 * DT)[3]
+    s_scaled = pc.xwt(7 * y1, 0.2 * y2, DT, 1 / 8, 2 * DT)[3]
+    np.testing.assert_allclose(s_scaled, s, rtol=1e-12)
+    raw = pc.xwt(y1, y2, DT, 1 / 8, 2 * DT, normalize=False)[3]
+    np.testing.assert_allclose(raw, s * y1.std() * y2.std(), rtol=1e-12)
+    freq = pc.xwt(y1, y2, DT, 1 / 8, 2 * DT)[2]
+    Pk = (pc.ar1_spectrum(freq * DT, pc.ar1(y1)[0]) * pc.ar1_spectrum(freq * DT, pc.ar1(y2)[0])) ** 0.5
+    np.testing.assert_allclose(s, Pk * 2.995732273553991, rtol=1e-12)

@@ -22,8 +22,9 @@ constexpr Entry kEntries[] = {
     {"modwt_syn", &Options::modwt_syn, 0, 1},
 };
 
-Options& mutable_options() {
-  static Options opts = [] {
+// Process defaults: the environment, read once (immutable afterwards).
+const Options& env_options() {
+  static const Options opts = [] {
     Options o;
     for (const Entry& e : kEntries) {
       char env[64] = "WTMI_";
@@ -39,28 +40,37 @@ Options& mutable_options() {
   }();
   return opts;
 }
+
+// What wtmi_set_option changes: the CALLING thread's copy.  A launch reads the options of
+// the thread issuing it, so a test or A/B script that overrides one on its thread can never
+// race (or tear) a launch issued concurrently by another thread.
+Options& thread_options() {
+  thread_local Options opts = env_options();
+  return opts;
+}
 }  // namespace
 
-const Options& options() { return mutable_options(); }
+const Options& options() { return thread_options(); }
 
 }  // namespace wtmi
 
 // Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
-// wct_min_rows, wct_dec_rows, modwt_syn).  0 on success, -1 unknown name or out of range.  Applies to launches
-// issued after the call; not to be called while another thread is launching.
+// wct_min_rows, wct_dec_rows, modwt_syn) for the CALLING thread.  0 on success, -1 unknown
+// name or out of range.  Applies to launches this thread issues after the call; other
+// threads keep their own values (the process defaults come from WTMI_<NAME>).
 extern "C" int wtmi_set_option(const char* name, long long value) {
   if (!name) return wtmi::kErrArg;
   for (const auto& e : wtmi::kEntries) {
     if (strcmp(name, e.name) == 0) {
       if (value < e.lo || value > e.hi) return wtmi::kErrArg;
-      wtmi::mutable_options().*(e.field) = static_cast<int>(value);
+      wtmi::thread_options().*(e.field) = static_cast<int>(value);
       return wtmi::kOk;
     }
   }
   return wtmi::kErrArg;
 }
 
-// Current value of an option, or -1 for an unknown name.
+// The calling thread's value of an option, or -1 for an unknown name.
 extern "C" long long wtmi_get_option(const char* name) {
   if (!name) return -1;
   for (const auto& e : wtmi::kEntries)

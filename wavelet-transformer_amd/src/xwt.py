@@ -116,8 +116,9 @@ def run_xwt_batch(xwt_data_list: List[DataForXWT], normalize: bool = True
             g2, _, _ = transforms._ar1_from_moments(mh2[k, 4], mh2[k, 5], int(mh2[k, 6]))
             Pk1 = transforms.ar1_spectrum(freqs * dt, g1)
             Pk2 = transforms.ar1_spectrum(freqs * dt, g2)
-            # sigma1 sigma2 of the raw series (pycwt keeps them through normalisation)
-            signif.append(mh1[k, 1] * mh2[k, 1] * (Pk1 * Pk2) ** 0.5 * chi)
+            # the reference calls pycwt.xwt with its default normalize=True whatever run_xwt's
+            # own flag (src/xwt.py:93-101), and pycwt then resets std1 = std2 = 1
+            signif.append((Pk1 * Pk2) ** 0.5 * chi)
         signif = np.stack(signif)
         period = 1 / freqs
         coi = transforms.cone_of_influence(n0, dt, mother)

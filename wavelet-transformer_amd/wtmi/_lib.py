@@ -79,7 +79,8 @@ def load() -> C.CDLL:
 
 
 def set_option(name: str, value: int) -> int:
-    """Set a launch option (include/wtmi.h); returns the previous value."""
+    """Set a launch option for the calling thread (include/wtmi.h: thread-local, so it never
+    races a launch on another thread); returns the previous value."""
     old = get_option(name)
     call("wtmi_set_option", name.encode(), int(value))
     return old
@@ -93,7 +94,8 @@ def get_option(name: str) -> int:
 
 
 class option:
-    """Context manager: ``with _lib.option("cwt_prune", 0): ...`` (tests / A/B scripts)."""
+    """Context manager: ``with _lib.option("cwt_prune", 0): ...`` (tests / A/B scripts).
+    Affects only launches issued by the calling thread inside the block."""
 
     def __init__(self, name: str, value: int):
         self.name, self.value = name, value

@@ -5,14 +5,23 @@ Every series (CWT, MODWT, DWT) and every pair (XWT / WCT) is independent
 rank runs the kernels on its own device with no collective on the data path.  The
 only cross-rank traffic is optional: a host-side gather of results to rank 0 for a
 consumer that wants them in one place, and the max-over-ranks of a timing.
+
+Process groups: an RCCL group (backend "nccl" on ROCm) has no CPU transport, so the
+host-side gather runs over a gloo side group created once from the same ranks
+(``host_group``), and scalar reductions use the group's own device.  Under a gloo (or
+"cpu:gloo,cuda:nccl") group everything stays on the host.
 """
 
 from __future__ import annotations
 
+import threading
 from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
+
+_HOST_GROUPS: dict = {}
+_HOST_LOCK = threading.Lock()
 
 
 def shard_range(batch: int, rank: int, world: int):
@@ -31,29 +40,70 @@ def run_sharded(x: torch.Tensor, fn: Callable[[torch.Tensor], torch.Tensor], ran
     return fn(x[s:e])
 
 
+def _has_cpu_transport(group) -> bool:
+    return "gloo" in str(dist.get_backend(group)).lower()
+
+
+def host_group(group=None):
+    """A process group that can carry CPU tensors among the ranks of `group`: the group
+    itself under gloo, else a gloo side group made once (collective: every rank of `group`
+    reaches the first call together, as they do inside ``gather_to_rank0``)."""
+    if _has_cpu_transport(group):
+        return group
+    key = id(group) if group is not None else None
+    with _HOST_LOCK:
+        g = _HOST_GROUPS.get(key)
+        if g is None:
+            ranks = None if group is None else dist.get_process_group_ranks(group)
+            g = dist.new_group(ranks=ranks, backend="gloo")
+            _HOST_GROUPS[key] = g
+    return g
+
+
 def gather_to_rank0(local: torch.Tensor, batch: int, group=None) -> Optional[torch.Tensor]:
     """Host-side gather of per-rank result blocks into the global batch order on rank 0.
 
-    Blocks are moved to host memory first, so the gather never touches the GPUs'
-    data path (works over gloo; with RCCL only the small host copies travel)."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    Each rank copies its block to host memory (D2H) and the blocks travel over a gloo
+    group (``host_group``): nothing of the data path goes through RCCL, under either
+    backend.  Returns the [batch, ...] host tensor on rank 0, None elsewhere."""
+    hg = host_group(group)
+    world = dist.get_world_size(hg)
+    rank = dist.get_rank(hg)
     host = local.detach().to("cpu").contiguous()
     per = -(-batch // world)
+    s, e = shard_range(batch, rank, world)
+    if host.shape[0] != e - s:
+        raise ValueError(f"rank {rank} holds {host.shape[0]} rows, its shard is {e - s}")
     pad_shape = (per,) + tuple(host.shape[1:])
     buf = torch.zeros(pad_shape, dtype=host.dtype)
     buf[: host.shape[0]] = host
     out = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, out, dst=0, group=group)
+    dist.gather(buf, out, dst=dist.get_global_rank(hg, 0) if hg is not None else 0, group=hg)
     if rank != 0:
         return None
     return torch.cat(out, dim=0)[:batch]
 
 
-def max_over_ranks(seconds: float, device: Optional[torch.device] = None) -> float:
-    """Max of a wall time over all ranks (the bench's timed region)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+def _reduce_device(group=None) -> torch.device:
+    if _has_cpu_transport(group) or not torch.cuda.is_available():
+        return torch.device("cpu")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def max_over_ranks(seconds: float, group=None) -> float:
+    """Max of a wall time over all ranks (the bench's timed region); a host tensor under
+    gloo, a tensor on this rank's GPU under RCCL."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return seconds
-    t = torch.tensor([seconds], dtype=torch.float64, device=device or "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([seconds], dtype=torch.float64, device=_reduce_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def sum_over_ranks(value: float, group=None) -> float:
+    """Sum of a scalar over all ranks (units processed), on the same device rule."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=_reduce_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return float(t.item())

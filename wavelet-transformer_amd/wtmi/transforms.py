@@ -14,6 +14,7 @@ return device tensors; the single-series functions wrap them.
 from __future__ import annotations
 
 import math
+import os
 import threading
 from typing import Optional
 
@@ -22,8 +23,6 @@ import torch
 
 from . import ops
 from .wavelets import Morlet, as_filter_bank, as_morlet
-
-_dev_lock = threading.Lock()
 
 
 def device() -> torch.device:
@@ -226,7 +225,9 @@ def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95, wavelet="mo
     x2 = ops.affine(d2, a2, torch.float32)
     W12 = ops.xwt_morlet(x1, x2, sj, dt, wavelet.f0, want_w12=True)["w12"][0]
     mh1, mh2 = _np(m1)[0], _np(m2)[0]
-    std1, std2 = mh1[1], mh2[1]  # raw series' std, normalised or not
+    # pycwt resets std1 = std2 = 1 for normalised series (unit variance after the transform);
+    # the raw deviations scale the test only when normalize=False
+    std1, std2 = (1.0, 1.0) if normalize else (mh1[1], mh2[1])
     g1, _, _ = _ar1_from_moments(mh1[4], mh1[5], int(mh1[6]))
     g2, _, _ = _ar1_from_moments(mh2[4], mh2[5], int(mh2[6]))
     Pk1 = ar1_spectrum(freq * dt, g1)
@@ -337,26 +338,26 @@ def significance_from_histogram(wlc: np.ndarray, anyout: np.ndarray, maxscale: i
 
 _sig_cache: dict = {}
 _sig_cache_lock = threading.Lock()
+# WTMI_WCT_SIG_CACHE=0 turns the significance cache off process-wide (latency
+# measurements of the uncached Monte Carlo; callers' cache=True is then ignored)
+SIG_CACHE = os.environ.get("WTMI_WCT_SIG_CACHE", "1") != "0"
 
 
 def sig_cache_dir() -> str:
     """Directory of the persistent significance cache: $WTMI_CACHE_DIR, else
     ~/.cache/wtmi/wct_sig (pycwt keeps its own under the user cache dir)."""
-    import os
     root = os.environ.get("WTMI_CACHE_DIR") or os.path.join(os.path.expanduser("~"), ".cache", "wtmi")
     return os.path.join(root, "wct_sig")
 
 
 def _sig_cache_path(key) -> str:
     import hashlib
-    import os
     h = hashlib.sha256(repr(key).encode()).hexdigest()[:32]
     return os.path.join(sig_cache_dir(), f"sig95_{h}.npy")
 
 
 def sig_cache_load(key):
     """sig95 for a wct_significance argument key: process memory first, then disk."""
-    import os
     with _sig_cache_lock:
         if key in _sig_cache:
             return _sig_cache[key].copy()
@@ -375,7 +376,6 @@ def sig_cache_load(key):
 def sig_cache_store(key, sig95) -> None:
     """Keep sig95 in memory and on disk (atomic rename; a failed write only costs a
     recomputation later)."""
-    import os
     import tempfile
     with _sig_cache_lock:
         _sig_cache[key] = np.array(sig95, copy=True)
@@ -402,6 +402,7 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     wavelet = as_morlet(wavelet)
     if wavelet.deltaj0 <= 0:
         raise ValueError("wct_significance needs a Morlet(6) wavelet (deltaj0 defined)")
+    cache = cache and SIG_CACHE
     key = ("wct_significance", 1, float(al1), float(al2), float(dt), float(dj), float(s0), int(J),
            float(significance_level), wavelet.f0, int(mc_count), int(nbins), seed)
     if cache:
