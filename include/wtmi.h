@@ -44,6 +44,23 @@ int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
                     double f0, const double* sig_scale, long long sig_ld, float* out_w,
                     float* out_power, float* out_sig, void* workspace, void* stream);
 
+/* ---- CWT / XWT with any pycwt mother ------------------------------------------
+ * The same transforms for the other mothers of the reference's MOTHER_DICT
+ * (src/xwt.py:29-34, src/wct.py:36-41, constants/results_configs.py:53-58):
+ * mother 0 = Morlet(f0 = param) (exactly wtmi_cwt_morlet / wtmi_xwt_morlet), 1 = Paul(m = param),
+ * 2 = DOG(m = param) (pycwt MexicanHat = DOG(2)); orders 1..40.  pycwt's filter
+ * sqrt(s w_1 N) conj(psi_hat(s w_k)) is evaluated in-register (full transforms: the band
+ * pruning is Morlet's).  Rows up to 16384 samples for mothers 1 and 2 (-2 above).          */
+int wtmi_cwt_mother(const float* x, long long ld, long long batch, long long n0,
+                    const double* affine, const double* scales, int n_scales, double dt,
+                    int mother, double param, const double* sig_scale, long long sig_ld,
+                    float* out_w, float* out_power, float* out_sig, void* workspace, void* stream);
+int wtmi_xwt_mother(const float* x1, const float* x2, long long ld, long long batch,
+                    long long n0, const double* affine1, const double* affine2,
+                    const double* scales, int n_scales, double dt, int mother, double param,
+                    const double* sig_scale, long long sig_ld, float* out_w12, float* out_power,
+                    float* out_sig, float* out_u, float* out_v, void* workspace, void* stream);
+
 /* Device scratch a CWT (pair = 0) or XWT (pair = 1) call needs: 0 for n0 <= 16384 (one
  * workgroup holds a row; workspace may be NULL), else the four-step long-row path's
  * spectra and work rows (bounded: series and scales are processed in chunks of about

@@ -85,6 +85,74 @@ class Morlet:
         return convolve2d(T, win[:, np.newaxis], "same")
 
 
+class Paul:
+    """Paul mother wavelet of order m, pycwt ``mothers.Paul`` (Torrence & Compo 1998,
+    Table 1).  psi_ft(f) = 2^m / sqrt(m (2m-1)!) f^m exp(-f) H(f); Fourier wavelength
+    4 pi / (2m + 1); e-folding time sqrt(2) s (``coi`` = sqrt(2)); dofmin 2; no ``smooth``
+    (pycwt defines it for Morlet only).  Reached through ``MOTHER_DICT["paul"]``
+    (reference src/xwt.py:29-34, src/wct.py:36-41, constants/results_configs.py:53-58)."""
+
+    name = "Paul"
+
+    def __init__(self, m: int = 4):
+        self.m = int(m)
+        self.dofmin = 2
+        if self.m == 4:
+            self.cdelta, self.gamma, self.deltaj0 = 1.132, 1.17, 1.50
+        else:
+            self.cdelta = self.gamma = self.deltaj0 = -1
+
+    def psi_ft(self, f):
+        f = np.asarray(f, dtype=float)
+        norm = 2 ** self.m / np.sqrt(self.m * np.prod(np.arange(2, 2 * self.m, dtype=float)))
+        return norm * np.where(f > 0, f, 0.0) ** self.m * np.exp(-np.where(f > 0, f, 0.0)) * (f > 0)
+
+    def flambda(self):
+        return 4 * np.pi / (2 * self.m + 1)
+
+    def coi(self):
+        return np.sqrt(2)
+
+
+class DOG:
+    """Derivative-of-Gaussian mother wavelet of order m, pycwt ``mothers.DOG``
+    (m = 2: the Mexican hat, pycwt ``MexicanHat``).  psi_ft(f) = -i^m / sqrt(Gamma(m + 1/2))
+    f^m exp(-f^2 / 2); Fourier wavelength 2 pi / sqrt(m + 1/2); e-folding time sqrt(2) s
+    (``coi`` = 1/sqrt(2)); dofmin 1; no ``smooth``."""
+
+    name = "DOG"
+
+    def __init__(self, m: int = 2):
+        self.m = int(m)
+        self.dofmin = 1
+        if self.m == 2:
+            self.cdelta, self.gamma, self.deltaj0 = 3.541, 1.43, 1.40
+        elif self.m == 6:
+            self.cdelta, self.gamma, self.deltaj0 = 1.966, 1.37, 0.97
+        else:
+            self.cdelta = self.gamma = self.deltaj0 = -1
+
+    def psi_ft(self, f):
+        from scipy.special import gamma
+        f = np.asarray(f, dtype=float)
+        return -(1j ** self.m) / np.sqrt(gamma(self.m + 0.5)) * f ** self.m * np.exp(-0.5 * f ** 2)
+
+    def flambda(self):
+        return 2 * np.pi / np.sqrt(self.m + 0.5)
+
+    def coi(self):
+        return 1 / np.sqrt(2)
+
+
+class MexicanHat(DOG):
+    """pycwt ``mothers.MexicanHat``: DOG of order 2."""
+
+    name = "Mexican Hat"
+
+    def __init__(self):
+        super().__init__(2)
+
+
 def rect(x: int, normalize: bool = False) -> np.ndarray:
     """Boxcar with half-weight end points (pycwt ``helpers.rect``)."""
     X = np.zeros(x)

@@ -13,7 +13,6 @@ vectors).  Only the resulting figure signatures (tests/figsig.figure_signature) 
 written; no reference code is stored.
 """
 
-import ast
 import json
 import logging
 import os
@@ -32,23 +31,18 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 import figsig  # noqa: E402
 from oracle import dwt_spec  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import refpin  # noqa: E402
+
 REF = os.environ.get("WTMI_REFERENCE", "/root/reference")
 OUT = os.path.join(ROOT, "tests", "golden", "plot_signatures.json")
 
 
 def extract(rel, names, ns):
-    """Execute the named top-level defs / assignments of a reference file in ns."""
-    tree = ast.parse(open(os.path.join(REF, rel)).read())
-    keep = []
-    for node in tree.body:
-        if isinstance(node, ast.FunctionDef) and node.name in names:
-            keep.append(node)
-        elif isinstance(node, ast.Assign) and isinstance(node.targets[0], ast.Name) \
-                and node.targets[0].id in names:
-            keep.append(node)
-    found = {getattr(n, "name", None) or n.targets[0].id for n in keep}
-    assert found == set(names), (rel, set(names) - found)
-    exec(compile(ast.Module(body=keep, type_ignores=[]), rel, "exec"), ns)
+    """Execute the named top-level defs / assignments of a reference file in ns -- only
+    after each segment's SHA-256 matches its pin (scripts/refpin.py, scripts/refpins.json)."""
+    mod = refpin.pinned_module(REF, rel, names)
+    exec(compile(mod, rel, "exec"), ns)
     return ns
 
 

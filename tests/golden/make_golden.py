@@ -40,11 +40,11 @@ class _NullLog:
 
 
 def load_functions(path, names):
-    src = open(path).read()
-    tree = ast.parse(src)
-    keep = [n for n in tree.body
-            if isinstance(n, (ast.FunctionDef, ast.ClassDef)) and n.name in names]
-    mod = ast.Module(body=keep, type_ignores=[])
+    """The named reference definitions, executed only after each segment's SHA-256 matches
+    its pin (scripts/refpin.py, scripts/refpins.json)."""
+    sys.path.insert(0, os.path.join(HERE, "..", "..", "scripts"))
+    import refpin
+    mod = refpin.pinned_module(REF, os.path.relpath(path, REF), sorted(names))
     ns = {"np": np, "npt": np.typing if hasattr(np, "typing") else None,
           "pywt": pywt, "convolve1d": convolve1d, "dataclass": dataclass,
           "field": field, "Dict": Dict, "Type": Type, "logger": _NullLog(),

@@ -149,10 +149,24 @@ def test_every_caller_attribute_exists(modules):
     assert absent_in_ref <= {("dwt", "smooth_signal")}, absent_in_ref
 
 
-def test_unsupported_mother_raises():
-    from wtmi.wavelets import Paul, as_morlet
-    with pytest.raises(ValueError, match="only Morlet"):
-        as_morlet(Paul())
+def test_mothers_resolve_and_coherence_needs_morlet():
+    """Every MOTHER_DICT value is a transformable mother (CWT / XWT kernels, mother ids of
+    include/wtmi.h); the coherence needs Morlet.smooth, which pycwt defines for Morlet
+    only -- pycwt.wct raises AttributeError there, and so does as_morlet (also a ValueError)."""
+    from wtmi.wavelets import DOG, MexicanHat, Morlet, Paul, as_morlet, as_mother, kernel_mother
+    assert kernel_mother(Morlet(6)) == (0, 6.0)
+    assert kernel_mother(Paul()) == (1, 4.0)
+    assert kernel_mother(DOG()) == (2, 2.0) == kernel_mother(MexicanHat())
+    assert kernel_mother("mexicanhat") == (2, 2.0)
+    for name in ("paul", "DOG", "mexicanhat"):
+        assert as_mother(name.lower()) is not None
+    for w in (Paul(), DOG(), MexicanHat()):
+        with pytest.raises(AttributeError, match="smooth"):
+            as_morlet(w)
+        with pytest.raises(ValueError):
+            as_morlet(w)
+    with pytest.raises(ValueError):
+        as_mother("haar")
 
 
 def test_run_cwt_unknown_kwarg_raises_typeerror(modules):

@@ -193,3 +193,23 @@ def test_xwt_significance_sigma_reset():
     freq = pc.xwt(y1, y2, DT, 1 / 8, 2 * DT)[2]
     Pk = (pc.ar1_spectrum(freq * DT, pc.ar1(y1)[0]) * pc.ar1_spectrum(freq * DT, pc.ar1(y2)[0])) ** 0.5
     np.testing.assert_allclose(s, Pk * 2.995732273553991, rtol=1e-12)
+
+
+@pytest.mark.parametrize("mother", [pc.Paul(4), pc.DOG(2), pc.DOG(3), pc.MexicanHat(), pc.Paul(2)])
+def test_other_mothers_known_answers(mother):
+    """pycwt's Paul / DOG restated (oracle/pycwt_spec.py): unit energy of psi_hat (the
+    Torrence & Compo normalisation, int |psi_hat|^2 dw = 1, which every pycwt mother meets),
+    and the Fourier wavelength: the CWT of a sinusoid of period P peaks at the scale whose
+    flambda * s is nearest P (A.6.2 for these mothers, within one dj = 1/24 step)."""
+    w = np.linspace(-60, 60, 240001)
+    e = np.sum(np.abs(mother.psi_ft(w)) ** 2) * (w[1] - w[0])
+    np.testing.assert_allclose(e, 1.0, rtol=1e-6)
+    n, P = 2048, 64.0
+    t = np.arange(n)
+    x = np.sin(2 * np.pi * t / P)
+    W, sj, freqs, coi, _, _ = pc.cwt(x, 1.0, 1 / 24, 2.0, 24 * 7, mother)
+    pw = (np.abs(W[:, n // 4: 3 * n // 4]) ** 2).mean(axis=1)  # T&C's (unrectified) power
+    j = int(np.argmax(pw))
+    period = 1 / freqs
+    assert abs(np.log2(period[j] / P)) <= 1 / 24, (period[j], P)
+    np.testing.assert_allclose(coi[1] / coi[0], 3.0)  # (n0/2 - |t - (n0-1)/2|) slope

@@ -109,6 +109,8 @@ struct Options {
   int wct_min_rows = 0;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least (0 = by batch)
   int wct_dec_rows = 0;     // WTMI_WCT_DEC_ROWS: decimated scale rows per phase A workgroup (0 = by batch)
   int modwt_syn = 1;        // WTMI_MODWT_SYN: 1 hybrid synthesis (low levels via LDS), 0 MODE 3 only
+  int wct_wide = 1;         // WTMI_WCT_WIDE: windows of union band N >> e take the spectral route
+                            // from e >= wct_wide (1..3); 0 = never (time path)
 };
 const Options& options();
 

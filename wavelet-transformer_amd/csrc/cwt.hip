@@ -9,7 +9,9 @@
 // each scale row is an analytic-filter multiply + in-LDS inverse FFT + a fused
 // epilogue writing any of {W (complex64), |W|^2, |W|^2 / signif_j} (cross mode:
 // {W1 W2*, |W1 W2*|^2, ratio, phase arrows u = sin(angle), v = cos(angle)}).
-// The Morlet filter is evaluated in-register: no filter bank is read from HBM.
+// The Morlet filter is evaluated in-register: no filter bank is read from HBM.  The same
+// kernels instantiated with VAR = 1 serve pycwt's other mothers (Paul, DOG / Mexican hat:
+// mother_filter, full transforms -- the band pruning is Morlet's).
 #include "cwt_common.hpp"
 #include "long_path.hpp"
 
@@ -157,9 +159,11 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const double s = a.scales[j0 + i];
-    const cpx mp = morlet_params(s, a.dt, P::N);
+    cpx mp = morlet_params(s, a.dt, P::N);
+    if constexpr (VAR == 1)  // log2(sqrt(2 pi s / dt) / N) + the mother's normalisation
+      mp.y = static_cast<float>(log2(sqrt(2.0 * kPi * s / a.dt) / static_cast<double>(P::N)) + a.mlnorm);
     const float sg = a.sigscale ? static_cast<float>(a.sigscale[b * a.sig_ld + j0 + i]) : 0.f;
-    const int code = NBUF == 1 ? row_code<LOGN>(s, a.dt, a.f0, a.prune) : 0;
+    const int code = (NBUF == 1 && VAR == 0) ? row_code<LOGN>(s, a.dt, a.f0, a.prune) : 0;
     prm_tab[i] = make_float4(mp.x, mp.y, sg, static_cast<float>(code));
   }
 
@@ -211,12 +215,20 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
       if (jj < j1 - j0) q = min(q, static_cast<int>(prm_tab[jj].w));
     }
     cpx v[16];
-    inverse_row<LOGN, NBUF, TWL>(v, X, prm, f0, q, my, bufstride, tw, t, par, twl);
+    auto inverse = [&](const cpx (&Xs)[16]) {
+      if constexpr (VAR == 1) {
+        mother_filter<LOGN>(v, Xs, prm, a, t);
+        fft_row<LOGN, 1, NBUF, TWL>(v, my, bufstride, tw, t, par, twl);
+      } else {
+        inverse_row<LOGN, NBUF, TWL>(v, Xs, prm, f0, q, my, bufstride, tw, t, par, twl);
+      }
+    };
+    inverse(X);
     if constexpr (MODE == 1) {
       cpx w1[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) w1[m] = v[m];
-      inverse_row<LOGN, NBUF, TWL>(v, X2, prm, f0, q, my, bufstride, tw, t, par, twl);
+      inverse(X2);
 #pragma unroll
       for (int m = 0; m < 16; ++m) v[m] = cmul(w1[m], cconj(v[m]));
     }
@@ -244,7 +256,7 @@ __global__ void __launch_bounds__(256) cwt_direct_kernel(CwtArgs a, int N) {
   const double s = a.scales[j];
   const double alpha = s * 2.0 * kPi / (N * a.dt);
   // pycwt's sqrt(s * ftfreqs[1] * N): fftfreq(2)[1] = -1/2, so a 2-point row is NaN there too
-  const double c = N == 2 ? __builtin_nan("") : sqrt(2.0 * kPi * s / a.dt) * 0.75112554446494248286 / N;
+  const double lc = N == 2 ? __builtin_nan("") : log2(sqrt(2.0 * kPi * s / a.dt) / N) + a.mlnorm;
   double2 w[2] = {make_double2(0, 0), make_double2(0, 0)};
   for (int which = 0; which < (MODE == 1 ? 2 : 1); ++which) {
     const float* row = (which ? a.x2 : a.x) + b * a.ld;
@@ -261,12 +273,12 @@ __global__ void __launch_bounds__(256) cwt_direct_kernel(CwtArgs a, int N) {
         xi += val * sn;
       }
       const int kk = k < N / 2 ? k : k - N;
-      const double e = alpha * kk - a.f0;
-      const double psi = c * exp(-0.5 * e * e);
+      const double2 psi = mother_psi_d(alpha * kk, lc, a);
       double sn, cs;
       sincospi(2.0 * ((static_cast<long long>(k) * tpos) % N) / N, &sn, &cs);
-      acc_re += psi * (xr * cs - xi * sn);
-      acc_im += psi * (xr * sn + xi * cs);
+      const double yr = xr * cs - xi * sn, yi = xr * sn + xi * cs;  // X[k] e^{2 pi i k t / N}
+      acc_re += psi.x * yr - psi.y * yi;
+      acc_im += psi.x * yi + psi.y * yr;
     }
     w[which] = make_double2(acc_re, acc_im);
   }
@@ -322,7 +334,8 @@ static int launch_fft_cwt(CwtArgs& a, hipStream_t st) {
   a.nchunks = nch;
   a.chunk = chunk;
   // 2: band-pruned rows and narrowed first passes; 1: band-pruned rows only; 0: full FFTs
-  a.prune = options().cwt_prune;
+  // (other mothers: full FFTs -- the band criteria are the Morlet filter's)
+  a.prune = VAR == 1 ? 0 : options().cwt_prune;
   const long long grid = a.batch * nch;
   if (grid > 0x7fffffffll) return kErrUnsupported;
   hipLaunchKernelGGL((cwt_morlet_kernel<LOGN, NBUF, MODE, VAR>), dim3(static_cast<unsigned>(grid)),
@@ -342,9 +355,9 @@ static int dispatch(CwtArgs& a, hipStream_t st) {
                        0, st, a, N);
     return launch_status();
   }
-#define WTMI_CASE(L) \
-  case L:            \
-    return launch_fft_cwt<L, 1, MODE>(a, st);
+#define WTMI_CASE(L)                                                                     \
+  case L:                                                                                \
+    return a.mother ? launch_fft_cwt<L, 1, MODE, 1>(a, st) : launch_fft_cwt<L, 1, MODE>(a, st);
   switch (logn) {
     WTMI_CASE(4) WTMI_CASE(5) WTMI_CASE(6) WTMI_CASE(7) WTMI_CASE(8) WTMI_CASE(9)
     WTMI_CASE(10) WTMI_CASE(11) WTMI_CASE(12) WTMI_CASE(13) WTMI_CASE(14)
@@ -358,11 +371,11 @@ static int dispatch(CwtArgs& a, hipStream_t st) {
 
 using namespace wtmi;
 
-extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
+extern "C" int wtmi_cwt_mother(const float* x, long long ld, long long batch, long long n0,
                                const double* affine, const double* scales, int n_scales,
-                               double dt, double f0, const double* sig_scale, long long sig_ld,
-                               float* out_w, float* out_power, float* out_sig, void* workspace,
-                               void* stream) {
+                               double dt, int mother, double param, const double* sig_scale,
+                               long long sig_ld, float* out_w, float* out_power, float* out_sig,
+                               void* workspace, void* stream) {
   if (!x || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
   if (sig_ld != 0 && sig_ld < n_scales) return kErrArg;
   if (!out_w && !out_power && !out_sig) return kErrArg;
@@ -370,6 +383,8 @@ extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, lo
   if (n0 > (1ll << kLongMaxLog)) return kErrUnsupported;
   if (n0 > (1 << 14) && !workspace) return kErrArg;
   CwtArgs a{};
+  if (!mother_consts(a, mother, param)) return kErrArg;
+  if (n0 > (1 << 14) && mother != 0) return kErrUnsupported;  // long rows: Morlet only
   a.x = x;
   a.ld = ld;
   a.batch = batch;
@@ -378,7 +393,6 @@ extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, lo
   a.affine = affine;
   a.scales = scales;
   a.dt = dt;
-  a.f0 = f0;
   a.sigscale = sig_scale;
   a.sig_ld = sig_ld;
   a.out_w = reinterpret_cast<cpx*>(out_w);
@@ -388,9 +402,18 @@ extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, lo
   return dispatch<0>(a, static_cast<hipStream_t>(stream));
 }
 
-extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long batch,
+extern "C" int wtmi_cwt_morlet(const float* x, long long ld, long long batch, long long n0,
+                               const double* affine, const double* scales, int n_scales,
+                               double dt, double f0, const double* sig_scale, long long sig_ld,
+                               float* out_w, float* out_power, float* out_sig, void* workspace,
+                               void* stream) {
+  return wtmi_cwt_mother(x, ld, batch, n0, affine, scales, n_scales, dt, 0, f0, sig_scale, sig_ld, out_w,
+                         out_power, out_sig, workspace, stream);
+}
+
+extern "C" int wtmi_xwt_mother(const float* x1, const float* x2, long long ld, long long batch,
                                long long n0, const double* affine1, const double* affine2,
-                               const double* scales, int n_scales, double dt, double f0,
+                               const double* scales, int n_scales, double dt, int mother, double param,
                                const double* sig_scale, long long sig_ld, float* out_w12,
                                float* out_power, float* out_sig, float* out_u, float* out_v,
                                void* workspace, void* stream) {
@@ -402,6 +425,8 @@ extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, l
   if (n0 > (1ll << kLongMaxLog)) return kErrUnsupported;
   if (n0 > (1 << 14) && !workspace) return kErrArg;
   CwtArgs a{};
+  if (!mother_consts(a, mother, param)) return kErrArg;
+  if (n0 > (1 << 14) && mother != 0) return kErrUnsupported;  // long rows: Morlet only
   a.x = x1;
   a.x2 = x2;
   a.ld = ld;
@@ -412,7 +437,6 @@ extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, l
   a.affine2 = affine2;
   a.scales = scales;
   a.dt = dt;
-  a.f0 = f0;
   a.sigscale = sig_scale;
   a.sig_ld = sig_ld;
   a.out_w = reinterpret_cast<cpx*>(out_w12);
@@ -422,4 +446,14 @@ extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, l
   a.out_v = out_v;
   if (n0 > (1 << 14)) return batch && n_scales ? cwt_long(a, true, workspace, static_cast<hipStream_t>(stream)) : kOk;
   return dispatch<1>(a, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int wtmi_xwt_morlet(const float* x1, const float* x2, long long ld, long long batch,
+                               long long n0, const double* affine1, const double* affine2,
+                               const double* scales, int n_scales, double dt, double f0,
+                               const double* sig_scale, long long sig_ld, float* out_w12,
+                               float* out_power, float* out_sig, float* out_u, float* out_v,
+                               void* workspace, void* stream) {
+  return wtmi_xwt_mother(x1, x2, ld, batch, n0, affine1, affine2, scales, n_scales, dt, 0, f0, sig_scale,
+                         sig_ld, out_w12, out_power, out_sig, out_u, out_v, workspace, stream);
 }

@@ -28,7 +28,49 @@ struct CwtArgs {
   int nchunks, chunk;
   int prune;             // 2: band-pruned rows + narrowed entry passes (row_code);
                          // 1: band-pruned rows only; 0: full FFTs
+  // Non-Morlet mothers (kernels instantiated with VAR = 1, full transforms only):
+  //   conj(psi_hat(f)) = (mcre + i mcim) gate(f) 2^(mA f^2 + mB f + mP log2|f| + lnorm),
+  // f = s w_k; gate 0: 1, 1: f > 0 (Paul), 2: sign(f) (DOG of odd order).  See mother_consts.
+  int mother;            // 0 Morlet (f0), 1 Paul (order m), 2 DOG (order m)
+  float mA, mB, mP, mcre, mcim;
+  int mgate;
+  double mlnorm;         // log2 of the mother's normalisation (Morlet: log2 pi^-1/4)
 };
+
+// Filter constants of a mother wavelet (pycwt 0.4.0b0 mothers.py: Paul.psi_ft, DOG.psi_ft).
+inline bool mother_consts(CwtArgs& a, int mother, double param) {
+  a.mother = mother;
+  a.mA = a.mB = a.mP = a.mcim = 0.f;
+  a.mcre = 1.f;
+  a.mgate = 0;
+  if (mother == 0) {  // Morlet(f0): the dedicated kernels; param = f0
+    a.f0 = param;
+    a.mlnorm = -0.25 * 1.6514961294723187;  // log2 pi^-1/4
+    return true;
+  }
+  const int m = static_cast<int>(param);
+  if (static_cast<double>(m) != param || m < 1 || m > 40) return false;
+  a.f0 = 0.0;
+  a.mP = static_cast<float>(m);
+  if (mother == 1) {  // Paul: 2^m / sqrt(m (2m-1)!) f^m e^-f H(f)
+    double lf = 0.0;  // log2 (2m-1)!
+    for (int k = 2; k < 2 * m; ++k) lf += log2(static_cast<double>(k));
+    a.mlnorm = m - 0.5 * (log2(static_cast<double>(m)) + lf);
+    a.mB = static_cast<float>(-1.4426950408889634);
+    a.mgate = 1;
+    return true;
+  }
+  if (mother == 2) {  // DOG: -i^m / sqrt(Gamma(m + 1/2)) f^m e^(-f^2/2); conj(-i^m)
+    a.mlnorm = -0.5 * lgamma(m + 0.5) / 0.6931471805599453;
+    a.mA = static_cast<float>(-0.5 * 1.4426950408889634);
+    a.mgate = (m & 1) ? 2 : 0;
+    static const float cre[4] = {-1.f, 0.f, 1.f, 0.f}, cim[4] = {0.f, 1.f, 0.f, -1.f};
+    a.mcre = cre[m & 3];
+    a.mcim = cim[m & 3];
+    return true;
+  }
+  return false;
+}
 
 constexpr double kPi = 3.14159265358979323846;
 constexpr float kLog2e = 1.44269504088896340736f;
@@ -222,6 +264,36 @@ __device__ __forceinline__ void morlet_filter_nz(cpx (&v)[16], const cpx (&X)[16
       v[m] = mkc(0.f, 0.f);
     }
   }
+}
+
+// v = X * conj(psi_hat(s w_k)) * sqrt(2 pi s / dt) / N for a non-Morlet mother (all 16 bins;
+// prm = (alpha, log2(sqrt(2 pi s / dt) / N) + lnorm), see mother_consts).
+template <int LOGN>
+__device__ __forceinline__ void mother_filter(cpx (&v)[16], const cpx (&X)[16], cpx prm, const CwtArgs& a,
+                                              int t) {
+  using P = FftPlan<LOGN>;
+  const cpx cst = mkc(a.mcre, a.mcim);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const float f = prm.x * static_cast<float>(t + (m < 8 ? m : m - 16) * P::NT);
+    const float e = fmaf(a.mA * f, f, fmaf(a.mB, f, fmaf(a.mP, __log2f(fabsf(f)), prm.y)));
+    float psi = __builtin_amdgcn_exp2f(e);
+    if (a.mgate == 1) psi = f > 0.f ? psi : 0.f;
+    if (a.mgate == 2) psi = f < 0.f ? -psi : psi;
+    v[m] = cmul(cscale(X[m], psi), cst);
+  }
+}
+
+// fp64 conj(psi_hat(f)) * 2^lc for the direct (n0 <= 8) kernels; lc as in mother_filter.
+__device__ __forceinline__ double2 mother_psi_d(double f, double lc, const CwtArgs& a) {
+  if (a.mother == 0) {
+    const double e = f - a.f0;
+    return make_double2(exp2(lc) * exp(-0.5 * e * e), 0.0);
+  }
+  if (f == 0.0 || (a.mgate == 1 && f < 0.0)) return make_double2(0.0, 0.0);
+  double psi = exp2(lc + a.mP * log2(fabs(f))) * exp(a.mother == 1 ? -f : -0.5 * f * f);
+  if (a.mgate == 2 && f < 0.0) psi = -psi;
+  return make_double2(psi * a.mcre, psi * a.mcim);
 }
 
 // Filtered bin t of a band-pruned row (thread t's m = 0 element, frequency index t >= 0).

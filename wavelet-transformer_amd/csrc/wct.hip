@@ -253,12 +253,28 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
 //   bit 4     spec  output row whose whole boxcar window has q >= 1: its coherence is made by
 //                   phase C from band spectra (no time-domain workspace round trip)
 //   bits 5-6  qw    that window's smallest regime (the union of the members' bands)
+//   bit 7     needW the row's smoothed spectra go to the wide-band workspace WB (phase C's wide
+//                   windows)
 //   bits 8-11 e     decimation of the row (wct_dec_kernel), 0 = none: W1, W2 have their spectra in
 //                   bins [0, M/2), M = N >> e, so the products |W1|^2, W1 conj(W2) have theirs in
 //                   (-M/2, M/2) and the forward transforms run on every (N/M)-th sample (length M)
+//   bits 12-15 ew   the row's smoothed band: both smoothed fields have their spectra in
+//                   [-Mw/2, Mw/2), Mw = N >> ew (the time Gaussian's cut-off, narrowed further by
+//                   the decimation's band); WB holds those Mw bins in FFT order
+//   bits 16-17 eu   wide output row (spec set, qw = 0): its window's union band is Mu = N >> eu
+//                   (eu in 1..3: the window holds rows of regime q = 0 but none of band ew = 0),
+//                   its coherence comes from the WB spectra through one band inverse of Mu bins
+//                   per field instead of the time-domain workspace
 enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5,
-             kPlanDecShift = 8 };
+             kPlanNeedW = 128, kPlanDecShift = 8, kPlanEwShift = 12, kPlanEuShift = 16 };
 __device__ __forceinline__ int plan_dec(int pl) { return (pl >> kPlanDecShift) & 15; }
+__device__ __forceinline__ int plan_ew(int pl) { return (pl >> kPlanEwShift) & 15; }
+__device__ __forceinline__ int plan_eu(int pl) { return (pl >> kPlanEuShift) & 3; }
+// wide windows need M = N >> 3 >= 32 bins (one band phasor per thread): LOGN >= 8; the
+// spectral boxcar keeps K rows in registers: K <= 24
+constexpr int kWideMinLogn = 8;
+constexpr int kWideMaxE = 3;
+constexpr int kWideMaxK = 24;
 
 // Decimated rows: M = N >> e with e in [kDecMinE(LOGN), LOGN - 5] -- M >= 32 (the band
 // inverse's phasor is one per thread), M <= 4096 (256-thread decimated groups) -- for full rows
@@ -274,6 +290,8 @@ __host__ __device__ constexpr int dec_rows_per_wg(int logm) { return logm >= 12 
 // schedule of wct_dec_kernel (after the plan's 3 S + 1 ints and S row-list ints):
 // [4 logm + 0] first row-list index, [+1] row count, [+2] first workgroup; [64] workgroups
 constexpr int kDecSched = 68;
+// [kSchedWide], [kSchedWide + 1]: first and last wide output row (first > last: none)
+constexpr int kSchedWide = 65;
 
 // e of row r (0: not decimated): the smallest M = 2^m >= 32 with psi negligible from bin M/2 on
 // (alpha M/2 - f0 >= kBandT, the band_regime criterion), if that M is at most N / 2.
@@ -285,6 +303,17 @@ __device__ __forceinline__ int dec_e(double s, double dt, double f0) {
   while (lm < LOGN && alpha * static_cast<double>(1 << (lm - 1)) - f0 < kBandT) ++lm;
   const int e = LOGN - lm;
   return (e >= dec_min_e<LOGN>() && e <= LOGN - kDecMinLogm) ? e : 0;
+}
+
+// Smoothed band exponent of a row: the largest e <= LOGN - 5 with the time Gaussian
+// F_k = exp(-(sn k)^2 / 2) below exp(-kBandT^2/2) for |k| >= N >> (e + 1) (the criterion of
+// smooth_regime, at every power of two).
+template <int LOGN>
+__device__ __forceinline__ int smooth_e(double sn) {
+  using P = FftPlan<LOGN>;
+  int e = 0;
+  while (e < LOGN - 5 && sn * static_cast<double>(P::N >> (e + 2)) >= kBandT) ++e;
+  return e;
 }
 
 template <int LOGN>
@@ -299,36 +328,66 @@ __device__ __forceinline__ int plan_q(const double* scales, int r, double dt, do
 // decimated rows' list (S ints) and schedule (kDecSched ints), see wct_dec_kernel.
 template <int LOGN>
 __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict__ scales, int S, double dt,
-                                                       double f0, int K, int prune, int dec, long long batch,
-                                                       int* __restrict__ plan, int* __restrict__ scratch) {
+                                                       double f0, int K, int prune, int dec, int wide,
+                                                       long long batch, int* __restrict__ plan,
+                                                       int* __restrict__ scratch) {
   __shared__ int last;
   if (threadIdx.x == 0) last = -1;
   const int LO = K / 2, HI = (K - 1) / 2;
-  int* qrow = scratch;  // regime | decimation e << 4
-  int* qwin = scratch + S;
-  for (int r = threadIdx.x; r < S; r += blockDim.x)
-    qrow[r] = (prune ? plan_q<LOGN>(scales, r, dt, f0) : 0) | ((dec ? dec_e<LOGN>(scales[r], dt, f0) : 0) << 4);
+  int* qrow = scratch;  // regime | decimation e << 4 | smoothed band ew << 8
+  int* qwin = scratch + S;  // window regime (>= 1: q window) | wide window eu << 4
+  constexpr bool kWide = LOGN >= kWideMinLogn;
+  for (int r = threadIdx.x; r < S; r += blockDim.x) {
+    const int ed = dec ? dec_e<LOGN>(scales[r], dt, f0) : 0;
+    const int es = (prune && kWide) ? smooth_e<LOGN>(scales[r] / dt * 2.0 * kPi / FftPlan<LOGN>::N) : 0;
+    qrow[r] = (prune ? plan_q<LOGN>(scales, r, dt, f0) : 0) | (ed << 4) | (max(es, ed) << 8);
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < S; i += blockDim.x) {  // window regime; -1: some member has q = 0
-    int qw = 3;
-    for (int r = max(0, i - LO); r <= min(S - 1, i + HI); ++r) qw = min(qw, qrow[r] & 15);
-    qwin[i] = (prune && qw >= 1) ? qw : -1;
+    int qw = 3, ew = 15;
+    for (int r = max(0, i - LO); r <= min(S - 1, i + HI); ++r) {
+      qw = min(qw, qrow[r] & 15);
+      ew = min(ew, qrow[r] >> 8);
+    }
+    // q windows keep phase C's band route; the other windows whose rows all have a smoothed
+    // band of at most N/2 take the wide route (union band N >> eu, capped at eu = 3: a wider
+    // band than needed is exact), the rest the time path
+    const int q_ok = (prune && qw >= 1) ? qw : -1;
+    const int eu = (prune && kWide && wide >= 1 && K <= kWideMaxK && q_ok < 1 && ew >= wide)
+                       ? min(ew, kWideMaxE) : 0;
+    qwin[i] = (q_ok >= 1 ? q_ok : 0) | (eu << 4);
   }
   __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
-    const int q = qrow[r] & 15, e = qrow[r] >> 4;
-    bool needT = false, needS = false;
+    const int q = qrow[r] & 15, e = (qrow[r] >> 4) & 15, ew = qrow[r] >> 8;
+    bool needT = false, needS = false, needW = false;
     for (int i = max(0, r - HI); i <= min(S - 1, r + LO); ++i) {  // outputs whose window holds r
-      if (qwin[i] >= 1) needS = true; else needT = true;
+      const int qwi = qwin[i] & 15, eui = (qwin[i] >> 4) & 3;
+      if (qwi >= 1) needS = true;
+      else if (eui >= 1) needW = true;
+      else needT = true;
     }
-    const int qw = qwin[r];
+    const int qw = qwin[r] & 15, eu = (qwin[r] >> 4) & 3;
     plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
-              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) | (e << kPlanDecShift);
-    if (qw < 1) atomicMax(&last, r);
+              (needW ? kPlanNeedW : 0) |
+              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) |
+              (eu >= 1 ? kPlanSpec | (eu << kPlanEuShift) : 0) |
+              (e << kPlanDecShift) | (ew << kPlanEwShift);
+    if (qw < 1 && eu < 1) atomicMax(&last, r);
   }
   __syncthreads();
   // decimated rows by class (LDS counters; the order of rows within a class is immaterial)
-  __shared__ int cnt[16], cur[16];
+  __shared__ int cnt[16], cur[16], wlo, whi;
+  if (threadIdx.x == 0) {
+    wlo = S;
+    whi = -1;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < S; r += blockDim.x)
+    if (plan_eu(plan[r])) {
+      atomicMin(&wlo, r);
+      atomicMax(&whi, r);
+    }
   if (threadIdx.x < 16) cnt[threadIdx.x] = cur[threadIdx.x] = 0;
   __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
@@ -350,6 +409,8 @@ __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict_
       wg += static_cast<int>((batch * cnt[lm] + dec_rows_per_wg(lm) - 1) / dec_rows_per_wg(lm));
     }
     sched[64] = wg;
+    sched[kSchedWide] = wlo;
+    sched[kSchedWide + 1] = whi;
   }
   __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
@@ -368,10 +429,31 @@ struct WctRowCtx {
   cpx* band;  // LDS: the band bins A1, A2 of a narrow row (2 * (N >> 8) complex)
   cpx* SB;    // smoothed band spectra [batch][S][2][NT] (index k + NT/2), see wct_plan
   const cpx* DY;  // decimated rows: W12's spectrum [batch][S][N/2] (M bins, wct_dec_kernel)
+  cpx* WB;        // wide-band smoothed spectra [batch][S][2][N/2] (Mw bins, plan bits ew)
   const int* plan;
   long long b;
   int j0;
 };
+
+// WB slot of row j, field f (0: Z = FFT(|W1|^2 + i |W2|^2) F / (N s), 1: FFT(W12) F / (N s)):
+// bins k in [-N/4, N/4) at index k + N/4; a row fills only its band [-Mw/2, Mw/2), Mw = N >> ew
+// (plan bits 12-15), and readers mask by that band.  wct_wide_boxcar later overwrites the slot
+// of a wide output row, bin by bin in place, with its window's sums (same index per bin).
+template <int LOGN>
+__device__ __forceinline__ cpx* wb_row(cpx* WB, long long b, int S, int j, int f) {
+  return WB + ((b * S + j) * 2 + f) * static_cast<long long>(FftPlan<LOGN>::N / 2) + FftPlan<LOGN>::N / 4;
+}
+__device__ __forceinline__ void wb_put(cpx* row, int mw, int k, cpx y) {
+  if (k >= -(mw >> 1) && k < (mw >> 1)) row[k] = y;
+}
+// The whole smoothed spectrum of a thread (bins t + (m < 8 ? m : m - 16) NT) into a WB slot.
+template <int LOGN>
+__device__ __forceinline__ void wb_put_full(cpx* row, int mw, const cpx (&v)[16], int t) {
+  using P = FftPlan<LOGN>;
+  asm volatile("" : "+v"(t));  // bin indices per row, not hoisted out of the scale loop (VGPRs)
+#pragma unroll
+  for (int m = 0; m < 16; ++m) wb_put(row, mw, t + (m < 8 ? m : m - 16) * P::NT, v[m]);
+}
 
 // Full-length inverse transform of a spectrum held in bins k in [-M/2, M/2), M = N >> E, stored
 // in FFT order (bin k at k mod M) in global memory: the band is shifted by H = M/2 to [0, M),
@@ -549,6 +631,11 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
         sb[t] = zy;
         sb[P::NT + t] = wy;
       }
+      if (valid && holder && (pl & kPlanNeedW)) {
+        const int mw = P::N >> plan_ew(pl);
+        wb_put(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 0), mw, k, zy);
+        wb_put(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 1), mw, k, wy);
+      }
       if (pl & kPlanNeedT) {
         const int slot = holder ? k + K0 : -1;
         smooth_from_band<LOGN, 2, TWL>(w1, wy, slot, my, tw, t, par, twl);
@@ -575,16 +662,29 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
     }
     fft_row<LOGN, -1, 1, TWL>(v, my, 0, tw, t, par, twl);
     if constexpr (Q == 0) {
+      const int pl = c.plan[c.j0 + (valid ? jl : r0)];
+      int pl_any = 0;  // workgroup-uniform (the smoothing transforms hold barriers)
+#pragma unroll
+      for (int gg = 0; gg < G::ROWS; ++gg)
+        if (r + gg < r1) pl_any |= c.plan[c.j0 + r + gg];
+      const bool wb = valid && (pl & kPlanNeedW);
+      const int mw = P::N >> plan_ew(pl);
       smooth_filter<LOGN>(v, smt.x, smt.y, t);
-      fft_row<LOGN, 1, 1, TWL>(v, my, 0, tw, t, par, twl);
-      // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
-      if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      if (wb) wb_put_full<LOGN>(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 0), mw, v, t);
+      if (pl_any & kPlanNeedT) {
+        fft_row<LOGN, 1, 1, TWL>(v, my, 0, tw, t, par, twl);
+        // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
+        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      }
       // the XWT-shaped outputs once z1 is dead (only W12 live: no spills around atan2)
       if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
       fft_row<LOGN, -1, 1, TWL>(w1, my, 0, tw, t, par, twl);
       smooth_filter<LOGN>(w1, smt.x, smt.y, t);
-      fft_row<LOGN, 1, 1, TWL>(w1, my, 0, tw, t, par, twl);
-      if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });
+      if (wb) wb_put_full<LOGN>(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 1), mw, w1, t);
+      if (pl_any & kPlanNeedT) {
+        fft_row<LOGN, 1, 1, TWL>(w1, my, 0, tw, t, par, twl);
+        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });
+      }
     } else {
       int zslot, wslot;
       const cpx zy = smooth_band_bin<LOGN, Q>(v, smt, t, zslot);
@@ -602,6 +702,12 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
         sb[ix] = zy;
         sb[P::NT + ix] = wy;
       }
+      if (valid && (pl & kPlanNeedW) && zslot >= 0) {  // bin k = slot - K0 (zslot == wslot)
+        constexpr int K0 = P::N >> (4 * Q + 1);
+        const int mw = P::N >> plan_ew(pl);
+        wb_put(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 0), mw, zslot - K0, zy);
+        wb_put(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 1), mw, zslot - K0, wy);
+      }
       if (pl_any & kPlanNeedT) {
         smooth_from_band<LOGN, Q, TWL>(w1, wy, wslot, my, tw, t, par, twl);
         if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
@@ -617,7 +723,8 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
 template <int LOGN, bool FULL, bool DEC>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB,
-                cpx* __restrict__ SB, const cpx* __restrict__ DY, const int* __restrict__ plan) {
+                cpx* __restrict__ SB, const cpx* __restrict__ DY, cpx* __restrict__ WB,
+                const int* __restrict__ plan) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
   constexpr int BAND_F4 = LOGN >= 12 ? (P::N >> 8) : 1;  // 2 * (N >> 8) complex
@@ -675,6 +782,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   c.band = reinterpret_cast<cpx*>(q_tab + G::MAXCHUNK);
   c.SB = SB;
   c.DY = DY;
+  c.WB = WB;
   c.plan = plan;
   c.b = b;
   c.j0 = j0;
@@ -736,6 +844,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
 template <int LOGN, int LOGM>
 __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restrict__ spec, cpx* __restrict__ TA,
                                           cpx* __restrict__ TB, cpx* __restrict__ SB, cpx* __restrict__ DY,
+                                          cpx* __restrict__ WB,
                                           const int* __restrict__ plan, const int* __restrict__ rows,
                                           const int* __restrict__ sched, int wl, cpx* lds) {
   using P = FftPlan<LOGN>;
@@ -807,8 +916,11 @@ __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restric
   const float sc = static_cast<float>(1.0 / (static_cast<double>(M) * s));
   constexpr int NTN = P::NT;  // SB row: bins k in [-NTN/2, NTN/2) at k + NTN/2
   const bool needT = valid && (pl & kPlanNeedT), needS = valid && (pl & kPlanNeedS);
+  const bool needW = valid && (pl & kPlanNeedW);
   cpx* trow = (f == 0 ? TA : TB) + row * static_cast<long long>(a.n0);
   cpx* sb = SB + row * 2ll * NTN + f * NTN;
+  cpx* wrow = WB + (row * 2 + f) * static_cast<long long>(P::N / 2) + P::N / 4;
+  const int mw = P::N >> plan_ew(pl);  // <= the row's M: ew >= its decimation e
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const int k = t + (m < 8 ? m : m - 16) * NTM;
@@ -817,6 +929,7 @@ __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restric
     int ix;
     if (needT && keep(m, ix)) trow[ix] = y;
     if (needS && k >= -NTN / 2 && k < NTN / 2) sb[k + NTN / 2] = y;
+    if (needW) wb_put(wrow, mw, k, y);
   }
   if constexpr (M < NTN) {  // band rows' SB bins outside (-M/2, M/2): zero, by the whole workgroup
     constexpr int Z = NTN - M;
@@ -838,22 +951,24 @@ template <int LOGN, int LOGM>
 __global__ void __launch_bounds__(512, 4) wct_dec_kernel(CwtArgs a, const cpx* __restrict__ spec,
                                                          cpx* __restrict__ TA, cpx* __restrict__ TB,
                                                          cpx* __restrict__ SB, cpx* __restrict__ DY,
-                                                         const int* __restrict__ plan) {
+                                                         cpx* __restrict__ WB, const int* __restrict__ plan) {
   __shared__ cpx lds[2 * dec_rows_per_wg(LOGM) * FftPlan<LOGM>::PADN];
   const int* rows = plan + 3 * a.S + 1;
   const int* sched = rows + a.S;
   const int w0 = sched[4 * LOGM + 2];
   const int nwg = (LOGM > kDecEngLogm ? sched[4 * (LOGM - 1) + 2] : sched[64]) - w0;
-  if (static_cast<int>(blockIdx.x) < nwg) dec_items<LOGN, LOGM>(a, spec, TA, TB, SB, DY, plan, rows, sched, blockIdx.x, lds);
+  if (static_cast<int>(blockIdx.x) < nwg)
+    dec_items<LOGN, LOGM>(a, spec, TA, TB, SB, DY, WB, plan, rows, sched, blockIdx.x, lds);
 }
 
 template <int LOGN, int LOGM>
 static int launch_dec_class(const CwtArgs& a, const cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY,
-                            const int* plan, hipStream_t st) {
+                            cpx* WB, const int* plan, hipStream_t st) {
   if constexpr (LOGM >= kDecEngLogm && LOGM <= LOGN - dec_min_e<LOGN>()) {
     // the class's workgroups are at most this many; the surplus exits at once
     const unsigned dg = static_cast<unsigned>((a.batch * a.S + dec_rows_per_wg(LOGM) - 1) / dec_rows_per_wg(LOGM));
-    hipLaunchKernelGGL((wct_dec_kernel<LOGN, LOGM>), dim3(dg), dim3(512), 0, st, a, spec, TA, TB, SB, DY, plan);
+    hipLaunchKernelGGL((wct_dec_kernel<LOGN, LOGM>), dim3(dg), dim3(512), 0, st, a, spec, TA, TB, SB, DY, WB,
+                       plan);
     return launch_status();
   }
   return kOk;
@@ -1036,10 +1151,118 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
   }
 }
 
+// Scale boxcar of the wide windows in the spectral domain (plan bits eu).  One thread = one bin
+// k in [-N/4, N/4) of one pair; it streams the rows of the wide windows down the scale axis
+// with the last K rows' (Z, W) bins in registers (a row contributes where its band [-Mw/2, Mw/2)
+// covers k) and, once output row i's window is complete, writes the window sums over row i's
+// own WB slot (bin k, in place: only this thread reads or writes index k, and row i's own bins
+// were read before).  Rows outside [0, S) and bins past a row's band count as zero.
+template <int K>
+__global__ void __launch_bounds__(256) wct_wide_boxcar(cpx* __restrict__ WB, long long batch, int N, int S,
+                                                       const int* __restrict__ plan) {
+  const int nb = N / 2;  // bins per slot
+  const long long tiles = (nb + 255) / 256;
+  const long long b = blockIdx.x / tiles;
+  const int u = static_cast<int>((blockIdx.x - b * tiles) * 256 + threadIdx.x);
+  if (u >= nb) return;
+  const int k = u - N / 4;
+  const int* rng = plan + 4 * S + 1 + kSchedWide;  // first / last wide output row (wct_plan_kernel)
+  const int i0 = rng[0], i1 = rng[1];
+  if (i0 > i1) return;
+  constexpr int LO = K / 2, HI = (K - 1) / 2;
+  const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
+  cpx* base = WB + b * S * 2ll * nb + u;  // row r field f at base + (2 r + f) nb
+  const int jlo = max(0, i0 - LO), jhi = min(S - 1, i1 + HI);
+  auto load = [&](int j, cpx& z, cpx& w) {  // row j's bins (zero past its band or the rows used)
+    z = w = mkc(0.f, 0.f);
+    if (j <= jhi) {
+      const int mw = N >> plan_ew(plan[j]);
+      if (k >= -(mw >> 1) && k < (mw >> 1)) {
+        z = base[(2ll * j) * nb];
+        w = base[(2ll * j + 1) * nb];
+      }
+    }
+  };
+  // rows are loaded D ahead of their use (D | K: the pending slot of row jb + q is q % D), so D
+  // rows of loads are in flight per thread; the sums' stores follow the loads they overtake
+  constexpr int D = (K % 6 == 0) ? 6 : (K % 5 == 0) ? 5 : (K % 4 == 0) ? 4 : (K % 3 == 0) ? 3 : (K % 2 == 0) ? 2 : 1;
+  cpx pz[D], pw[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(jlo + d, pz[d], pw[d]);
+  cpx rz[K], rw[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) rz[q] = rw[q] = mkc(0.f, 0.f);
+  // slot of row j: (j - jlo) % K; rows are taken K at a time so the slots index statically
+  for (int jb = jlo; jb <= jhi + HI; jb += K) {
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const int j = jb + q;
+      rz[q] = pz[q % D];
+      rw[q] = pw[q % D];
+      load(j + D, pz[q % D], pw[q % D]);
+      const int i = j - HI;  // its window [i - LO, i + HI] = rows j - K + 1 .. j
+      if (i >= i0 && i <= i1) {
+        const int pl = plan[i];
+        const int mu = N >> plan_eu(pl);
+        if (plan_eu(pl) && k >= -(mu >> 1) && k < (mu >> 1)) {
+          cpx sz = mkc(0.f, 0.f), sw = sz;
+#pragma unroll
+          for (int qq = 0; qq < K; ++qq) {  // row i - LO + qq sits in slot (q + 1 + qq) % K
+            const int slot = (q + 1 + qq) % K;
+            const float wq = (K > 1 && (qq == 0 || qq == K - 1)) ? 0.5f * wn : wn;
+            if (i - LO + qq >= jlo) {
+              sz = cfma(cpx{wq, wq}, rz[slot], sz);
+              sw = cfma(cpx{wq, wq}, rw[slot], sw);
+            }
+          }
+          base[(2ll * i) * nb] = sz;
+          base[(2ll * i + 1) * nb] = sw;
+        }
+      }
+    }
+  }
+}
+
+// Wide output rows (plan bits eu): the window sums of wct_wide_boxcar in the row's WB slot go
+// through one band inverse of Mu = N >> EU bins per field (shifted by H = Mu/2, entry pass
+// narrowed to NZ = 16 >> EU inputs) -- S1 + i S2 and S12 at every sample -- and WCT is written.
+// Replaces, for these rows, phase A's two inverse smoothing transforms per row, the 16-byte
+// time-domain workspace write and phase B's read of it.
+template <int LOGN, int EU, bool BUF, bool TWL>
+__device__ __forceinline__ void wct_wide_rows(const CwtArgs& a, const cpx* __restrict__ WB, long long b,
+                                              int j0, int r0, int r1, cpx* my, const cpx* tw, int g, int t,
+                                              int& par, const float4* twl, float* __restrict__ coh) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  using BG = BandGeom<LOGN, EU>;
+  static_assert(BG::Q == 0, "wide windows enter at pass 0");
+  for (int r = r0; r < r1; r += G::ROWS) {
+    const int jl = r + g;
+    const bool valid = jl < r1;
+    const int i = j0 + (valid ? jl : r0);
+    const cpx* zrow = WB + ((b * a.S + i) * 2) * static_cast<long long>(P::N / 2) + (P::N / 4 - BG::H);
+    cpx pre[8];
+    cpx v[16];
+    float den[16];
+#pragma unroll
+    for (int q = 0; q < BG::NZ; ++q) pre[q] = zrow[t + q * P::NT];  // shifted bin p -> k = p - H
+    band_ifft<LOGN, EU, TWL>(v, pre, my, tw, t, par, twl);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) den[m] = v[m].x * v[m].y;  // S1 S2
+#pragma unroll
+    for (int q = 0; q < BG::NZ; ++q) pre[q] = zrow[P::N / 2 + t + q * P::NT];
+    band_ifft<LOGN, EU, TWL>(v, pre, my, tw, t, par, twl);
+    if (valid) {
+      const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
+      put_row<LOGN, BUF>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
+    }
+  }
+}
+
 template <int LOGN, bool FULL>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
-    wct_phase_c(CwtArgs a, const cpx* __restrict__ SB, const int* __restrict__ plan, int K,
-                float* __restrict__ coh) {
+    wct_phase_c(CwtArgs a, const cpx* __restrict__ SB, const cpx* __restrict__ WB, const int* __restrict__ plan,
+                int K, float* __restrict__ coh) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
   constexpr bool BUF = FULL && P::NT >= kWave;
@@ -1070,9 +1293,10 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   int par = 0;
   __syncthreads();
   const int nrow = j1 - j0;
-  auto key = [&](int r) {
+  auto key = [&](int r) {  // 1, 2: q windows; 4 + eu: wide windows; 0: not phase C's
     const int pl = plan[j0 + r];
-    return (pl & kPlanSpec) ? ((pl >> kPlanQwShift) & 3) : 0;
+    if (!(pl & kPlanSpec)) return 0;
+    return plan_eu(pl) ? 4 + plan_eu(pl) : ((pl >> kPlanQwShift) & 3);
   };
   int r0 = 0;
   while (r0 < nrow) {
@@ -1084,6 +1308,11 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
       if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
         if (q == 2) wct_spec_rows<LOGN, 2, BUF, TWL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
       }
+    }
+    if constexpr (LOGN >= kWideMinLogn) {
+      if (q == 5) wct_wide_rows<LOGN, 1, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      if (q == 6) wct_wide_rows<LOGN, 2, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      if (q == 7) wct_wide_rows<LOGN, 3, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
     }
     r0 = r1;
   }
@@ -1103,8 +1332,8 @@ static int wct_dec_rows_per_wg(long long batch) {
 }
 
 template <int LOGN>
-static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY, int* plan, int K,
-                          float* coh, hipStream_t st) {
+static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY, cpx* WB, int* plan,
+                          int K, float* coh, hipStream_t st) {
   using G = WctGeom<LOGN>;
   {
     const long long items = 2 * a.batch;
@@ -1138,24 +1367,26 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   // decimated rows: full rows, pruning level 2, Morlet negative frequencies negligible
   const int dec = (a.prune >= 2 && a.n0 == (1 << LOGN) && LOGN >= kDecMinLogn && a.f0 >= kBandF0) ? 1 : 0;
   hipLaunchKernelGGL(wct_plan_kernel<LOGN>, dim3(1), dim3(256), 0, st, a.scales, a.S, a.dt, a.f0, K,
-                     a.prune, dec, a.batch, plan, plan + a.S + 1);
+                     a.prune, dec, options().wct_wide, a.batch, plan, plan + a.S + 1);
   int rc = launch_status();
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
   if (a.n0 != (1 << LOGN)) {
-    hipLaunchKernelGGL((wct_phase_a<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, plan);
+    hipLaunchKernelGGL((wct_phase_a<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
+                       plan);
     return launch_status();
   }
   // Full rows: the non-decimated rows' kernel, then (with decimated rows) their spectra and their
   // kernel.  (Running the first on a second stream beside the decimated work, and phase C beside
   // the decimated rows' kernel, measured a tie and 0.1 ms slower on C4: each saturates the CUs.)
-  hipLaunchKernelGGL((wct_phase_a<LOGN, true, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, plan);
+  hipLaunchKernelGGL((wct_phase_a<LOGN, true, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
+                     plan);
   if ((rc = launch_status()) != kOk) return rc;
   if constexpr (LOGN >= kDecMinLogn) {
     if (dec) {
       for (int lm = kDecMaxLogm; lm >= kDecEngLogm; --lm) {
         switch (lm) {
-#define WTMI_DC(LM) case LM: rc = launch_dec_class<LOGN, LM>(a, spec, TA, TB, SB, DY, plan, st); break;
+#define WTMI_DC(LM) case LM: rc = launch_dec_class<LOGN, LM>(a, spec, TA, TB, SB, DY, WB, plan, st); break;
           WTMI_DC(12) WTMI_DC(11) WTMI_DC(10) WTMI_DC(9) WTMI_DC(8)
 #undef WTMI_DC
           default: break;
@@ -1168,7 +1399,7 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
       if (ad.chunk > G::MAXCHUNK) ad.chunk = G::MAXCHUNK;
       ad.nchunks = (a.S + ad.chunk - 1) / ad.chunk;
       hipLaunchKernelGGL((wct_phase_a<LOGN, true, true>), dim3(static_cast<unsigned>(a.batch * ad.nchunks)),
-                         dim3(G::BLOCK), 0, st, ad, spec, TA, TB, SB, DY, plan);
+                         dim3(G::BLOCK), 0, st, ad, spec, TA, TB, SB, DY, WB, plan);
       return launch_status();
     }
   }
@@ -1177,14 +1408,14 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
 
 // Phase C over the chunk grid phase A used (a.nchunks / a.chunk as launch_phase_a set them).
 template <int LOGN>
-static int launch_phase_c(const CwtArgs& a, const cpx* SB, const int* plan, int K, float* coh,
+static int launch_phase_c(const CwtArgs& a, const cpx* SB, const cpx* WB, const int* plan, int K, float* coh,
                           hipStream_t st) {
   using G = WctGeom<LOGN>;
   const dim3 gd(static_cast<unsigned>(a.batch * a.nchunks));
   if (a.n0 == (1 << LOGN))
-    hipLaunchKernelGGL((wct_phase_c<LOGN, true>), gd, dim3(G::BLOCK), 0, st, a, SB, plan, K, coh);
+    hipLaunchKernelGGL((wct_phase_c<LOGN, true>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
   else
-    hipLaunchKernelGGL((wct_phase_c<LOGN, false>), gd, dim3(G::BLOCK), 0, st, a, SB, plan, K, coh);
+    hipLaunchKernelGGL((wct_phase_c<LOGN, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
   return launch_status();
 }
 
@@ -1382,7 +1613,8 @@ using namespace wtmi;
 
 // workspace = [T: batch x S x n0 float4][spectra: batch x 2 x N cpx]
 //             [band spectra: batch x S x 2 x N/16 cpx][decimated W12 spectra: batch x S x N/2 cpx,
-//             N >= 2^kDecMinLogn][plan: S + 1 int][plan scratch: 2 S int][decimated rows: S int]
+//             N >= 2^kDecMinLogn][wide-band spectra: batch x S x 2 x N/2 cpx, N >= 2^kWideMinLogn]
+//             [plan: S + 1 int][plan scratch: 2 S int][decimated rows: S int]
 //             [decimated schedule: kDecSched int]
 static long long wct_t_bytes(long long batch, long long n0, int n_scales) {
   const long long b = batch * n0 * static_cast<long long>(n_scales) * static_cast<long long>(sizeof(cpx));
@@ -1396,6 +1628,11 @@ static long long wct_sb_bytes(long long batch, long long n0, int n_scales) {
   const long long nt = wct_n(n0) / 16 > 0 ? wct_n(n0) / 16 : 1;
   return (batch * n_scales * 2 * nt * static_cast<long long>(sizeof(cpx)) + 255) & ~255ll;
 }
+// wide-band smoothed spectra WB: [batch][S][2][N/2] cpx (LOGN >= kWideMinLogn)
+static long long wct_wb_bytes(long long batch, long long n0, int n_scales) {
+  if (wct_n(n0) < (1ll << kWideMinLogn)) return 0;
+  return (batch * n_scales * wct_n(n0) * static_cast<long long>(sizeof(cpx)) + 255) & ~255ll;
+}
 static long long wct_dy_bytes(long long batch, long long n0, int n_scales) {
   if (wct_n(n0) < (1ll << kDecMinLogn) || wct_n(n0) != n0) return 0;  // decimated rows: full rows only
   return (batch * n_scales * (wct_n(n0) / 2) * static_cast<long long>(sizeof(cpx)) + 255) & ~255ll;
@@ -1405,7 +1642,8 @@ extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int
   if (batch < 0 || n0 < 0 || n_scales < 0) return -1;
   if (n0 > (1 << 14)) return wct_long_workspace_bytes(batch, n0, n_scales);
   return wct_t_bytes(batch, n0, n_scales) + wct_spec_bytes(batch, n0) + wct_sb_bytes(batch, n0, n_scales) +
-         wct_dy_bytes(batch, n0, n_scales) + 4ll * (4 * n_scales + 1 + kDecSched);
+         wct_dy_bytes(batch, n0, n_scales) + wct_wb_bytes(batch, n0, n_scales) +
+         4ll * (4 * n_scales + 1 + kDecSched);
 }
 
 extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
@@ -1458,10 +1696,12 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   ws += wct_sb_bytes(batch, n0, n_scales);
   cpx* DY = reinterpret_cast<cpx*>(ws);  // used only when wct_dy_bytes > 0 (launch_phase_a's dec)
   ws += wct_dy_bytes(batch, n0, n_scales);
+  cpx* WB = reinterpret_cast<cpx*>(ws);  // used only when wct_wb_bytes > 0 (wide windows)
+  ws += wct_wb_bytes(batch, n0, n_scales);
   int* plan = reinterpret_cast<int*>(ws);
   int rc;
   switch (logn) {
-#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, plan, boxcar, out_coh, st); break;
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, WB, plan, boxcar, out_coh, st); break;
     WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
     WTMI_A(12) WTMI_A(13) WTMI_A(14)
 #undef WTMI_A
@@ -1471,13 +1711,31 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   const int n0i = static_cast<int>(n0);
   auto phase_c = [&](hipStream_t cs) -> int {
     switch (logn) {
-#define WTMI_C(L) case L: return launch_phase_c<L>(a, SB, plan, boxcar, out_coh, cs);
+#define WTMI_C(L) case L: return launch_phase_c<L>(a, SB, WB, plan, boxcar, out_coh, cs);
       WTMI_C(4) WTMI_C(5) WTMI_C(6) WTMI_C(7) WTMI_C(8) WTMI_C(9) WTMI_C(10) WTMI_C(11)
       WTMI_C(12) WTMI_C(13) WTMI_C(14)
 #undef WTMI_C
       default: return kErrUnsupported;
     }
   };
+  // spectral boxcar of the wide windows (their sums over the output rows' WB slots)
+  if (wct_wb_bytes(batch, n0, n_scales) > 0 && a.prune >= 1 && boxcar <= kWideMaxK) {
+    const long long tiles = ((1ll << logn) / 2 + 255) / 256;
+    if (batch * tiles > 0x7fffffffll) return kErrUnsupported;
+    switch (boxcar) {
+#define WTMI_W(KK)                                                                                         \
+  case KK:                                                                                                 \
+    hipLaunchKernelGGL(wct_wide_boxcar<KK>, dim3(static_cast<unsigned>(batch * tiles)), dim3(256), 0, st, WB, \
+                       batch, 1 << logn, n_scales, plan);                                                 \
+    break;
+      WTMI_W(1) WTMI_W(2) WTMI_W(3) WTMI_W(4) WTMI_W(5) WTMI_W(6) WTMI_W(7) WTMI_W(8)
+      WTMI_W(9) WTMI_W(10) WTMI_W(11) WTMI_W(12) WTMI_W(13) WTMI_W(14) WTMI_W(15) WTMI_W(16)
+      WTMI_W(17) WTMI_W(18) WTMI_W(19) WTMI_W(20) WTMI_W(21) WTMI_W(22) WTMI_W(23) WTMI_W(24)
+#undef WTMI_W
+      default: break;
+    }
+    if ((rc = launch_status()) != kOk) return rc;
+  }
   // (phase B on a side stream beside phase C, fork/join by events, measured no faster:
   // C4 4.21-4.36 vs 4.23-4.24 ms -- phase C's workgroups hold the CUs, r02)
   if ((rc = phase_c(st)) != kOk) return rc;

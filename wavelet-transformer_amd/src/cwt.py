@@ -19,7 +19,7 @@ import numpy.typing as npt
 import torch
 
 from wtmi import ops, transforms
-from wtmi.wavelets import Morlet, as_morlet
+from wtmi.wavelets import Morlet, as_mother, kernel_mother
 from src.utils.wavelet_helpers import plot_cone_of_influence, plot_signficance_levels
 
 logger = logging.getLogger(__name__)
@@ -89,10 +89,10 @@ def run_cwt_batch(cwt_data_list: List[DataForCWT], normalize: bool = True,
     out: List[ResultsFromCWT] = [None] * len(cwt_data_list)
     groups: dict = {}
     for i, d in enumerate(cwt_data_list):
-        mother = as_morlet(d.mother_wavelet)
-        groups.setdefault((np.asarray(d.y_values).size, mother.f0), []).append(i)
-    for (n0, f0), idx in groups.items():
-        mother = as_morlet(cwt_data_list[idx[0]].mother_wavelet)
+        groups.setdefault((np.asarray(d.y_values).size, kernel_mother(d.mother_wavelet)), []).append(i)
+    for (n0, _), idx in groups.items():
+        # any pycwt mother (Morlet, Paul, DOG / MexicanHat), as pycwt.cwt takes them
+        mother = as_mother(cwt_data_list[idx[0]].mother_wavelet)
         y = transforms._to_dev(np.stack([np.asarray(cwt_data_list[i].y_values, dtype=np.float64)
                                          for i in idx]))
         mom_y = ops.series_moments(y)
@@ -116,8 +116,8 @@ def run_cwt_batch(cwt_data_list: List[DataForCWT], normalize: bool = True,
                                                     wavelet=mother)
                 rows.append(1.0 / signif)
             sig_scale = np.stack(rows)
-        res = ops.cwt_morlet(x32, sj, DT, mother.f0, sig_scale=sig_scale, want_w=False,
-                             want_power=True, want_sig=calculate_significance)
+        res = ops.cwt_morlet(x32, sj, DT, sig_scale=sig_scale, want_w=False, want_power=True,
+                             want_sig=calculate_significance, mother=mother)
         power = transforms._np(res["power"], np.float64)
         sig = transforms._np(res["sig"], np.float64) if calculate_significance else None
         coi = transforms.cone_of_influence(n0, DT, mother)

@@ -29,7 +29,7 @@ DT = 1 / 12
 DJ = 1 / 8
 S0 = 2 * DT
 MOTHER = "morlet"
-MOTHER_DICT = {  # only "morlet" is transformable; the others raise in run_wct
+MOTHER_DICT = {  # coherence needs Morlet.smooth: the others raise (AttributeError, as pycwt.wct)
     "morlet": Morlet(6),
     "paul": Paul(),
     "DOG": DOG(),

@@ -5,7 +5,11 @@ the significance ratio come from one pair-mode HIP kernel launch; the phase arro
 from a second launch at the scales pycwt.wct would use -- the reference passes
 ``delta_j=`` to ``wct`` which swallows it, so the phase runs at dj = 1/12
 (quirk B.5).  ``normalize=False`` raises NameError in the reference (B.7); here it
-returns the raw complex cross spectrum (documented deviation).
+returns the raw complex cross spectrum (documented deviation).  Non-Morlet mothers
+(``MOTHER_DICT["paul"]``, ``["DOG"]``, ``["mexicanhat"]``): the power and significance
+are pycwt.xwt's for that mother; the reference then fails inside pycwt.wct (only Morlet
+has ``smooth``), whereas here the phase is the angle of W1 W2* -- what pycwt.wct returns
+as aWCT, which needs no smoothing (documented deviation).
 """
 
 from __future__ import annotations
@@ -19,7 +23,7 @@ import numpy.typing as npt
 import torch
 
 from wtmi import ops, transforms
-from wtmi.wavelets import DOG, MexicanHat, Morlet, Paul, as_morlet
+from wtmi.wavelets import DOG, MexicanHat, Morlet, Paul, as_mother, kernel_mother
 from src.utils import wavelet_helpers
 from src.utils.wavelet_helpers import coi_polygon
 
@@ -29,7 +33,7 @@ DT = 1 / 12
 DJ = 1 / 8
 S0 = 2 * DT
 MOTHER = "morlet"
-MOTHER_DICT = {  # only "morlet" is transformable; the others raise in run_xwt
+MOTHER_DICT = {  # every key is transformable (the CWT kernels evaluate each mother's filter)
     "morlet": Morlet(6),
     "paul": Paul(),
     "DOG": DOG(),
@@ -89,15 +93,14 @@ def run_xwt_batch(xwt_data_list: List[DataForXWT], normalize: bool = True
     out: List[ResultsFromXWT] = [None] * len(xwt_data_list)
     groups: dict = {}
     for i, d in enumerate(xwt_data_list):
-        mother = as_morlet(d.mother_wavelet)
         n1, n2 = np.asarray(d.y1_values).size, np.asarray(d.y2_values).size
         if n1 != n2:
             raise ValueError("y1_values and y2_values must have the same length")
-        key = (n1, mother.f0, float(d.delta_t), float(d.delta_j), float(d.initial_scale),
-               tuple(d.levels))
+        key = (n1, kernel_mother(d.mother_wavelet), float(d.delta_t), float(d.delta_j),
+               float(d.initial_scale), tuple(d.levels))
         groups.setdefault(key, []).append(i)
-    for (n0, f0, dt, dj, s0, levels), idx in groups.items():
-        mother = as_morlet(xwt_data_list[idx[0]].mother_wavelet)
+    for (n0, _, dt, dj, s0, levels), idx in groups.items():
+        mother = as_mother(xwt_data_list[idx[0]].mother_wavelet)
         d1 = transforms._to_dev(np.stack([np.asarray(xwt_data_list[i].y1_values, dtype=np.float64)
                                           for i in idx]))
         d2 = transforms._to_dev(np.stack([np.asarray(xwt_data_list[i].y2_values, dtype=np.float64)
@@ -109,7 +112,7 @@ def run_xwt_batch(xwt_data_list: List[DataForXWT], normalize: bool = True
         sj, freqs = transforms.scales_for(n0, dt, dj, s0, -1, mother)
         mh1, mh2 = transforms._np(m1), transforms._np(m2)
         dof = mother.dofmin
-        chi = transforms._chi2_ppf(0.95, dof) / dof
+        chi = transforms._chi2_ppf(0.95, dof) / dof  # DOG: dofmin 1
         signif = []
         for k in range(len(idx)):
             g1, _, _ = transforms._ar1_from_moments(mh1[k, 4], mh1[k, 5], int(mh1[k, 6]))
@@ -123,19 +126,19 @@ def run_xwt_batch(xwt_data_list: List[DataForXWT], normalize: bool = True
         period = 1 / freqs
         coi = transforms.cone_of_influence(n0, dt, mother)
         if normalize:
-            r = ops.xwt_morlet(x1, x2, sj, dt, mother.f0, sig_scale=1.0 / signif,
-                               want_power=True, want_sig=True)
+            r = ops.xwt_morlet(x1, x2, sj, dt, sig_scale=1.0 / signif, want_power=True,
+                               want_sig=True, mother=mother)
             power = transforms._np(r["power"], np.float64)
             sig95 = transforms._np(r["sig"], np.float64)
             coi_plot = coi_polygon(coi, period, np.log2(levels[2]))
         else:
-            r = ops.xwt_morlet(x1, x2, sj, dt, mother.f0, want_w12=True)
+            r = ops.xwt_morlet(x1, x2, sj, dt, want_w12=True, mother=mother)
             power = transforms._np(r["w12"], np.complex128)
             sig95 = power / (np.ones([1, n0]) * signif[:, :, None])
             coi_plot = coi
         # phase: pycwt.wct(..., delta_j=...) runs at its default dj = 1/12 (quirk B.5)
         sj_p, _ = transforms.scales_for(n0, dt, 1 / 12, s0, -1, mother)
-        rp = ops.xwt_morlet(x1, x2, sj_p, dt, mother.f0, want_uv=True)
+        rp = ops.xwt_morlet(x1, x2, sj_p, dt, want_uv=True, mother=mother)
         u = transforms._np(rp["u"], np.float64)
         v = transforms._np(rp["v"], np.float64)
         for k, i in enumerate(idx):

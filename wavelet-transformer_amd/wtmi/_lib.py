@@ -26,6 +26,10 @@ _U64 = C.c_ulonglong
 PROTOTYPES = {
     "wtmi_cwt_morlet": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _F64, _F64, _P, _I64, _P, _P,
                                _P, _P, _P]),
+    "wtmi_cwt_mother": (_I32, [_P, _I64, _I64, _I64, _P, _P, _I32, _F64, _I32, _F64, _P, _I64, _P, _P,
+                               _P, _P, _P]),
+    "wtmi_xwt_mother": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _I32, _F64, _P, _I64,
+                               _P, _P, _P, _P, _P, _P, _P]),
     "wtmi_cwt_workspace_bytes": (_I64, [_I64, _I64, _I32, _I32]),
     "wtmi_xwt_morlet": (_I32, [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I32, _F64, _F64, _P, _I64,
                                _P, _P, _P, _P, _P, _P, _P]),

@@ -180,11 +180,23 @@ def _f64_arg(a, dev):
     return None if a is None else a.to(device=dev, dtype=torch.float64).contiguous()
 
 
+def _mother_args(mother, f0):
+    """(id, parameter) for wtmi_cwt_mother / wtmi_xwt_mother: None -> Morlet(f0); else a
+    wtmi / pycwt mother object or an (id, parameter) pair (wavelets.kernel_mother)."""
+    if mother is None:
+        return 0, float(f0)
+    if isinstance(mother, tuple):
+        return int(mother[0]), float(mother[1])
+    from .wavelets import kernel_mother
+    return kernel_mother(mother)
+
+
 def cwt_morlet(x: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
                affine: Optional[torch.Tensor] = None, sig_scale=None,
                want_w: bool = True, want_power: bool = False, want_sig: bool = False,
-               out_w: Optional[torch.Tensor] = None):
-    """Morlet CWT of every row of x (float32 [B, n0]) at the given scales.
+               out_w: Optional[torch.Tensor] = None, mother=None):
+    """CWT of every row of x (float32 [B, n0]) at the given scales: Morlet(f0), or the
+    pycwt mother ``mother`` (Paul / DOG / MexicanHat objects, wavelets.kernel_mother).
 
     Returns a dict with any of ``w`` (complex64 [B, S, n0]), ``power`` and ``sig``
     (float32 [B, S, n0], sig = power * sig_scale[j], or sig_scale[b, j] for a [B, S]
@@ -215,10 +227,13 @@ def cwt_morlet(x: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
         res["power"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
     if want_sig:
         res["sig"] = torch.empty((B, S, n0), dtype=torch.float32, device=dev)
+    mid, mpar = _mother_args(mother, f0)
+    if mid != 0 and n0 > 16384:
+        raise ValueError("non-Morlet mothers: series of at most 16384 samples")
     ws = _long_workspace(B, n0, S, 0, dev)
     with torch.cuda.device(dev):
-        _lib.call("wtmi_cwt_morlet", _ptr(x), x.stride(0), B, n0, _ptr(aff), _ptr(sc), S,
-                  float(dt), float(f0), _ptr(ss), sig_ld, _ptr(res.get("w")),
+        _lib.call("wtmi_cwt_mother", _ptr(x), x.stride(0), B, n0, _ptr(aff), _ptr(sc), S,
+                  float(dt), mid, mpar, _ptr(ss), sig_ld, _ptr(res.get("w")),
                   _ptr(res.get("power")), _ptr(res.get("sig")), _ptr(ws), _stream(dev))
     return res
 
@@ -250,9 +265,9 @@ def _pair_rows(x1, x2):
 
 def xwt_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
                affine1=None, affine2=None, sig_scale=None, want_w12=False, want_power=False,
-               want_sig=False, want_uv=False):
+               want_sig=False, want_uv=False, mother=None):
     """Cross-wavelet outputs of row pairs: any of w12 (complex64), power, sig, u, v.
-    sig_scale: [S] or per-pair [B, S] (1 / signif)."""
+    sig_scale: [S] or per-pair [B, S] (1 / signif).  mother: as cwt_morlet."""
     x1, x2 = _pair_rows(x1, x2)
     B, n0 = x1.shape
     S = _n_scales(scales)
@@ -276,10 +291,13 @@ def xwt_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     if want_uv:
         res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
         res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
+    mid, mpar = _mother_args(mother, f0)
+    if mid != 0 and n0 > 16384:
+        raise ValueError("non-Morlet mothers: series of at most 16384 samples")
     ws = _long_workspace(B, n0, S, 1, dev)
     with torch.cuda.device(dev):
-        _lib.call("wtmi_xwt_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
-                  _ptr(sc), S, float(dt), float(f0), _ptr(ss), sig_ld, _ptr(res.get("w12")),
+        _lib.call("wtmi_xwt_mother", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
+                  _ptr(sc), S, float(dt), mid, mpar, _ptr(ss), sig_ld, _ptr(res.get("w12")),
                   _ptr(res.get("power")), _ptr(res.get("sig")), _ptr(res.get("u")),
                   _ptr(res.get("v")), _ptr(ws), _stream(dev))
     return res

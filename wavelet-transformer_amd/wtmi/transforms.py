@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .wavelets import Morlet, as_filter_bank, as_morlet
+from .wavelets import Morlet, as_filter_bank, as_morlet, as_mother
 
 
 def device() -> torch.device:
@@ -106,7 +106,7 @@ def ar1(x):
 def significance(signal, dt, scales, sigma_test=0, alpha=None, significance_level=0.95,
                  dof=-1, wavelet="morlet"):
     """pycwt ``significance`` for sigma_test == 0 (the only form the reference uses)."""
-    wavelet = as_morlet(wavelet)
+    wavelet = as_mother(wavelet)
     try:
         n0 = len(signal)
     except TypeError:
@@ -172,18 +172,19 @@ def standardize_series(series, detrend=True, standardize=True, remove_mean=False
 # -------------------------------------------------------------------------- CWT
 def cwt_batch(x: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wavelet="morlet", *, affine=None,
               sig_scale=None, want_w=True, want_power=False, want_sig=False):
-    """Batched Morlet CWT of device rows; returns (dict of device tensors, sj, freqs)."""
-    wavelet = as_morlet(wavelet)
+    """Batched CWT of device rows (any pycwt mother: Morlet, Paul, DOG / MexicanHat);
+    returns (dict of device tensors, sj, freqs)."""
+    wavelet = as_mother(wavelet)
     n0 = x.shape[-1]
     sj, freqs = scales_for(n0, dt, dj, s0, J, wavelet)
-    res = ops.cwt_morlet(x, sj, dt, wavelet.f0, affine=affine, sig_scale=sig_scale,
-                         want_w=want_w, want_power=want_power, want_sig=want_sig)
+    res = ops.cwt_morlet(x, sj, dt, affine=affine, sig_scale=sig_scale, want_w=want_w,
+                         want_power=want_power, want_sig=want_sig, mother=wavelet)
     return res, sj, freqs
 
 
 def cwt(signal, dt, dj=1 / 12, s0=-1, J=-1, wavelet="morlet", freqs=None):
-    """pycwt-compatible ``cwt``: (W, sj, freqs, coi, signal_ft, ftfreqs)."""
-    wavelet = as_morlet(wavelet)
+    """pycwt-compatible ``cwt``: (W, sj, freqs, coi, signal_ft, ftfreqs), any pycwt mother."""
+    wavelet = as_mother(wavelet)
     sig = np.asarray(signal)
     n0 = sig.size
     if freqs is not None:
@@ -194,7 +195,7 @@ def cwt(signal, dt, dj=1 / 12, s0=-1, J=-1, wavelet="morlet", freqs=None):
     xd = _to_dev(sig).reshape(1, -1)
     x32 = ops.affine(xd, torch.tensor([[0.0, 0.0, 1.0]], dtype=torch.float64, device=xd.device),
                      torch.float32)
-    W = ops.cwt_morlet(x32, sj, dt, wavelet.f0, want_w=True)["w"][0]
+    W = ops.cwt_morlet(x32, sj, dt, want_w=True, mother=wavelet)["w"][0]
     N = int(2 ** np.ceil(np.log2(n0)))
     ft = torch.fft.fft(xd[0], n=N)
     ftfreqs = 2 * np.pi * np.fft.fftfreq(N, dt)
@@ -211,8 +212,8 @@ def _pair_norm(y1, y2):
 
 def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95, wavelet="morlet",
         normalize=True):
-    """pycwt-compatible ``xwt``: (W12, coi, freq, signif)."""
-    wavelet = as_morlet(wavelet)
+    """pycwt-compatible ``xwt``: (W12, coi, freq, signif), any pycwt mother."""
+    wavelet = as_mother(wavelet)
     d1, d2, m1, m2 = _pair_norm(y1, y2)
     n0 = d1.shape[1]
     sj, freq = scales_for(n0, dt, dj, s0, J, wavelet)
@@ -223,7 +224,7 @@ def xwt(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, significance_level=0.95, wavelet="mo
         a1 = a2 = ident
     x1 = ops.affine(d1, a1, torch.float32)
     x2 = ops.affine(d2, a2, torch.float32)
-    W12 = ops.xwt_morlet(x1, x2, sj, dt, wavelet.f0, want_w12=True)["w12"][0]
+    W12 = ops.xwt_morlet(x1, x2, sj, dt, want_w12=True, mother=wavelet)["w12"][0]
     mh1, mh2 = _np(m1)[0], _np(m2)[0]
     # pycwt resets std1 = std2 = 1 for normalised series (unit variance after the transform);
     # the raw deviations scale the test only when normalize=False

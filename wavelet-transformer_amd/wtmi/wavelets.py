@@ -45,22 +45,13 @@ class Morlet:
         return f"Morlet(f0={self.f0:g})"
 
 
-class _Unsupported:
-    """Descriptor of a pycwt mother wavelet the engine does not transform (only the Morlet
-    Fourier filter is built into the CWT kernels).  Carries pycwt 0.4.0b0's constants so
-    that the reference's ``MOTHER_DICT`` keys exist (src/xwt.py:29-34, src/wct.py:36-41);
-    passing one to a transform raises ValueError, as for any non-Morlet wavelet."""
-
-    name = "unsupported"
-
-    def __repr__(self):
-        return f"{type(self).__name__}(m={self.m})"
-
-
-class Paul(_Unsupported):
-    """pycwt ``Paul(m=4)``: flambda = 4 pi / (2m + 1), coi = sqrt(2)."""
+class Paul:
+    """pycwt ``Paul(m=4)``: conj(psi_hat(f)) = 2^m / sqrt(m (2m-1)!) f^m e^-f H(f) (real),
+    flambda = 4 pi / (2m + 1), coi = sqrt(2), dofmin 2.  Transformed by the CWT / XWT kernels
+    (mother id 1, include/wtmi.h); pycwt gives it no ``smooth``, so coherence raises."""
 
     name = "Paul"
+    kernel_id = 1
 
     def __init__(self, m: int = 4):
         self.m, self.dofmin = m, 2
@@ -69,17 +60,29 @@ class Paul(_Unsupported):
         else:
             self.cdelta = self.gamma = self.deltaj0 = -1
 
+    def psi_ft(self, f):
+        f = np.asarray(f, dtype=float)
+        fp = np.where(f > 0, f, 0.0)
+        norm = 2 ** self.m / np.sqrt(self.m * np.prod(np.arange(2, 2 * self.m, dtype=float)))
+        return norm * fp ** self.m * np.exp(-fp) * (f > 0)
+
     def flambda(self) -> float:
         return (4 * np.pi) / (2 * self.m + 1)
 
     def coi(self) -> float:
         return np.sqrt(2)
 
+    def __repr__(self):
+        return f"Paul(m={self.m})"
 
-class DOG(_Unsupported):
-    """pycwt ``DOG(m=2)`` (derivative of Gaussian): flambda = 2 pi / sqrt(m + 1/2)."""
+
+class DOG:
+    """pycwt ``DOG(m=2)`` (derivative of Gaussian): psi_hat(f) = -i^m / sqrt(Gamma(m + 1/2))
+    f^m e^(-f^2/2), flambda = 2 pi / sqrt(m + 1/2), coi = 1/sqrt(2), dofmin 1.  Transformed by
+    the CWT / XWT kernels (mother id 2); no ``smooth`` (pycwt), so coherence raises."""
 
     name = "DOG"
+    kernel_id = 2
 
     def __init__(self, m: int = 2):
         self.m, self.dofmin = m, 1
@@ -90,11 +93,19 @@ class DOG(_Unsupported):
         else:
             self.cdelta = self.gamma = self.deltaj0 = -1
 
+    def psi_ft(self, f):
+        from math import gamma
+        f = np.asarray(f, dtype=float)
+        return -(1j ** self.m) / np.sqrt(gamma(self.m + 0.5)) * f ** self.m * np.exp(-0.5 * f ** 2)
+
     def flambda(self) -> float:
         return (2 * np.pi / np.sqrt(self.m + 0.5))
 
     def coi(self) -> float:
         return 1 / np.sqrt(2)
+
+    def __repr__(self):
+        return f"{type(self).__name__}(m={self.m})"
 
 
 class MexicanHat(DOG):
@@ -106,8 +117,17 @@ class MexicanHat(DOG):
         super().__init__(2)
 
 
+Morlet.kernel_id = 0
+
+
+class NoSmoothError(AttributeError, ValueError):
+    """A coherence (Morlet.smooth) was asked of a mother pycwt gives no ``smooth`` method:
+    pycwt.wct raises AttributeError there; the ValueError base keeps the older contract."""
+
+
 def as_morlet(wavelet) -> Morlet:
-    """Accept a wtmi/pycwt Morlet object, the string 'morlet', or None (Morlet(6))."""
+    """Accept a wtmi/pycwt Morlet object, the string 'morlet', or None (Morlet(6)).  The
+    coherence paths need it: pycwt defines ``smooth`` for Morlet only."""
     if wavelet is None:
         return Morlet(6)
     if isinstance(wavelet, Morlet):
@@ -115,11 +135,47 @@ def as_morlet(wavelet) -> Morlet:
     if isinstance(wavelet, str):
         if wavelet.lower() == "morlet":
             return Morlet(6)
-        raise ValueError(f"unsupported mother wavelet {wavelet!r}: only Morlet is implemented")
-    if hasattr(wavelet, "f0") and type(wavelet).__name__.lower() == "morlet":
-        m = Morlet(float(wavelet.f0))
-        return m
-    raise ValueError(f"unsupported mother wavelet {wavelet!r}: only Morlet is implemented")
+    elif hasattr(wavelet, "f0") and type(wavelet).__name__.lower() == "morlet":
+        return Morlet(float(wavelet.f0))
+    if isinstance(wavelet, (str, Paul, DOG)) or type(wavelet).__name__ in ("Paul", "DOG", "MexicanHat"):
+        raise NoSmoothError(f"{wavelet!r} has no attribute 'smooth': the wavelet coherence "
+                            "needs Morlet (pycwt defines Morlet.smooth only)")
+    raise ValueError(f"unsupported mother wavelet {wavelet!r}")
+
+
+_MOTHER_NAMES = {"morlet": lambda: Morlet(6), "paul": lambda: Paul(4), "dog": lambda: DOG(2),
+                 "mexicanhat": MexicanHat}
+
+
+def as_mother(wavelet):
+    """Any mother the CWT / XWT kernels transform: wtmi or pycwt Morlet / Paul / DOG /
+    MexicanHat objects (duck-typed on the class name and ``f0`` / ``m``), their lower-case
+    names, or None (Morlet(6))."""
+    if wavelet is None:
+        return Morlet(6)
+    if isinstance(wavelet, (Morlet, Paul, DOG)):
+        return wavelet
+    if isinstance(wavelet, str):
+        key = wavelet.lower().replace(" ", "").replace("_", "")
+        if key in _MOTHER_NAMES:
+            return _MOTHER_NAMES[key]()
+        raise ValueError(f"unsupported mother wavelet {wavelet!r}")
+    cls = type(wavelet).__name__
+    if cls == "Morlet" and hasattr(wavelet, "f0"):
+        return Morlet(float(wavelet.f0))
+    if cls == "Paul" and hasattr(wavelet, "m"):
+        return Paul(int(wavelet.m))
+    if cls == "MexicanHat":
+        return MexicanHat()
+    if cls == "DOG" and hasattr(wavelet, "m"):
+        return DOG(int(wavelet.m))
+    raise ValueError(f"unsupported mother wavelet {wavelet!r}")
+
+
+def kernel_mother(wavelet):
+    """(mother id, parameter) of the C ABI's wtmi_cwt_mother / wtmi_xwt_mother."""
+    w = as_mother(wavelet)
+    return (0, float(w.f0)) if isinstance(w, Morlet) else (w.kernel_id, float(w.m))
 
 
 _FILTERS = None
