@@ -447,12 +447,27 @@ __device__ __forceinline__ void wb_put(cpx* row, int mw, int k, cpx y) {
   if (k >= -(mw >> 1) && k < (mw >> 1)) row[k] = y;
 }
 // The whole smoothed spectrum of a thread (bins t + (m < 8 ? m : m - 16) NT) into a WB slot.
+// Rows owned by whole waves (NT >= 64) store through a wave-uniform buffer descriptor: one
+// offset VGPR, the per-m bin offsets as immediates (no 64-bit address per store).
 template <int LOGN>
 __device__ __forceinline__ void wb_put_full(cpx* row, int mw, const cpx (&v)[16], int t) {
   using P = FftPlan<LOGN>;
   asm volatile("" : "+v"(t));  // bin indices per row, not hoisted out of the scale loop (VGPRs)
+  if constexpr (P::NT >= kWave) {
+    // slot start as the descriptor base (buffer offsets are unsigned); |k| < Mw/2 <= N/4 = 4 NT
+    // leaves only m = 0..3 and 12..15
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row - P::N / 4);
 #pragma unroll
-  for (int m = 0; m < 16; ++m) wb_put(row, mw, t + (m < 8 ? m : m - 16) * P::NT, v[m]);
+    for (int m = 0; m < 16; ++m) {
+      if (m >= 4 && m < 12) continue;
+      const int off = (m < 8 ? m : m - 16) * P::NT;
+      const int k = t + off;
+      if (k >= -(mw >> 1) && k < (mw >> 1)) buf_st(v[m], r, 8 * t, 8 * (off + P::N / 4));
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) wb_put(row, mw, t + (m < 8 ? m : m - 16) * P::NT, v[m]);
+  }
 }
 
 // Full-length inverse transform of a spectrum held in bins k in [-M/2, M/2), M = N >> E, stored
@@ -718,9 +733,14 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
   }
 }
 
-// DEC: this launch runs the decimated rows (plan e > 0) only, else every other row (two
-// launches over the same chunk grid, so that each kernel gets its own register budget).
-template <int LOGN, bool FULL, bool DEC>
+// KIND: which rows this launch runs -- 0 the full-band rows (regime 0, not decimated), 1 the
+// other non-decimated rows (regimes 1, 2), 2 the decimated rows (plan e > 0).  Separate
+// launches over the same chunk grid, so that each row kind gets its own kernel's register
+// budget (one kernel for kinds 0 and 1 spilled 128 bytes per lane on LOGN 13, kind 0 alone 48).
+template <int LOGN> __device__ __forceinline__ int phase_a_kind(int pl) {
+  return plan_dec(pl) > 0 ? 2 : ((pl & kPlanQ) == 0 ? 0 : 1);
+}
+template <int LOGN, bool FULL, int KIND>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB,
                 cpx* __restrict__ SB, const cpx* __restrict__ DY, cpx* __restrict__ WB,
@@ -746,7 +766,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   cpx* my = lds + g * P::PADN;
   {  // any rows of this launch's kind in the chunk?  (uniform: every thread reads the same plan)
     bool any = false;
-    for (int r = j0; r < j1; ++r) any |= (plan_dec(plan[r]) > 0) == DEC;
+    for (int r = j0; r < j1; ++r) any |= phase_a_kind<LOGN>(plan[r]) == KIND;
     if (!any) return;
   }
 
@@ -754,7 +774,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     const int pl = plan[j0 + i];
     // run key: the regime, or 4 + e for decimated rows
     q_tab[i] = plan_dec(pl) > 0 ? 4 + plan_dec(pl) : (pl & kPlanQ);
-    if (DEC) continue;  // decimated rows need no filter tables
+    if (KIND == 2) continue;  // decimated rows need no filter tables
     const double s = a.scales[j0 + i];
     prm_tab[i] = morlet_params(s, a.dt, P::N);
     const double sn = s / a.dt * 2.0 * kPi / P::N;  // (s/dt) * (2 pi / N)
@@ -794,7 +814,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     int r1 = r0 + 1;
     while (r1 < nrow && q_tab[r1] == q) ++r1;
     if (q >= 4) {  // decimated rows (full rows only)
-      if constexpr (DEC && FULL && LOGN >= kDecMinLogn) {
+      if constexpr (KIND == 2 && FULL && LOGN >= kDecMinLogn) {
         switch (q - 4) {
 #define WTMI_DR(EE)                                                                     \
   case EE:                                                                              \
@@ -806,13 +826,15 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
           default: break;
         }
       }
-    } else if (DEC) {
+    } else if (KIND == 2) {
     } else if (q == 0) {
-      if (a.prune && a.f0 >= kBandF0 && P::NT >= 16)  // negative frequencies dropped: half the bins
-        wct_rows<LOGN, FULL, 0, TWL, 8>(a, c, r0, r1, my, tw, g, t, par, twl);
-      else
-        wct_rows<LOGN, FULL, 0, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);
-    } else {
+      if constexpr (KIND == 0) {
+        if (a.prune && a.f0 >= kBandF0 && P::NT >= 16)  // negative frequencies dropped: half the bins
+          wct_rows<LOGN, FULL, 0, TWL, 8>(a, c, r0, r1, my, tw, g, t, par, twl);
+        else
+          wct_rows<LOGN, FULL, 0, TWL>(a, c, r0, r1, my, tw, g, t, par, twl);
+      }
+    } else if constexpr (KIND == 1) {
       if constexpr (P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
         if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
           if (q >= 2) {
@@ -945,8 +967,15 @@ __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restric
   }
 }
 
-// One launch per decimation class (the class sizes are known on the device only: each launch
-// covers the largest possible class, workgroups past the schedule's count exit at once).
+constexpr long long kDecGrid = 2048;  // 4 workgroups of 512 per CU on 256 CUs, twice
+// grid-stride from M = 2^9 on (up to 8 rows per item); the 16-row items of M = 256 keep one item
+// per workgroup (their class grid is at most batch x S / 16, and the loop spilled 60 B per lane)
+constexpr int kDecStrideLogm = 9;
+
+// One launch per decimation class (the class sizes are known on the device only).  The grid is
+// capped (kDecGrid) and strides over the class's workgroup items: a grid sized for the largest
+// possible class (batch x S items at M = 4096) was mostly workgroups that read the schedule
+// and exit.
 template <int LOGN, int LOGM>
 __global__ void __launch_bounds__(512, 4) wct_dec_kernel(CwtArgs a, const cpx* __restrict__ spec,
                                                          cpx* __restrict__ TA, cpx* __restrict__ TB,
@@ -957,16 +986,25 @@ __global__ void __launch_bounds__(512, 4) wct_dec_kernel(CwtArgs a, const cpx* _
   const int* sched = rows + a.S;
   const int w0 = sched[4 * LOGM + 2];
   const int nwg = (LOGM > kDecEngLogm ? sched[4 * (LOGM - 1) + 2] : sched[64]) - w0;
-  if (static_cast<int>(blockIdx.x) < nwg)
+  if constexpr (LOGM >= kDecStrideLogm) {
+    for (int wl = blockIdx.x; wl < nwg; wl += gridDim.x) {
+      if (wl != static_cast<int>(blockIdx.x)) __syncthreads();  // the previous item's LDS reads are done
+      dec_items<LOGN, LOGM>(a, spec, TA, TB, SB, DY, WB, plan, rows, sched, wl, lds);
+    }
+  } else if (static_cast<int>(blockIdx.x) < nwg) {
     dec_items<LOGN, LOGM>(a, spec, TA, TB, SB, DY, WB, plan, rows, sched, blockIdx.x, lds);
+  }
 }
+
 
 template <int LOGN, int LOGM>
 static int launch_dec_class(const CwtArgs& a, const cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY,
                             cpx* WB, const int* plan, hipStream_t st) {
   if constexpr (LOGM >= kDecEngLogm && LOGM <= LOGN - dec_min_e<LOGN>()) {
-    // the class's workgroups are at most this many; the surplus exits at once
-    const unsigned dg = static_cast<unsigned>((a.batch * a.S + dec_rows_per_wg(LOGM) - 1) / dec_rows_per_wg(LOGM));
+    // the class's workgroup items are at most this many; the grid strides over them
+    const long long most = (a.batch * a.S + dec_rows_per_wg(LOGM) - 1) / dec_rows_per_wg(LOGM);
+    const long long cap = LOGM >= kDecStrideLogm ? kDecGrid : most;
+    const unsigned dg = static_cast<unsigned>(most < cap ? most : cap);
     hipLaunchKernelGGL((wct_dec_kernel<LOGN, LOGM>), dim3(dg), dim3(512), 0, st, a, spec, TA, TB, SB, DY, WB,
                        plan);
     return launch_status();
@@ -1259,7 +1297,10 @@ __device__ __forceinline__ void wct_wide_rows(const CwtArgs& a, const cpx* __res
   }
 }
 
-template <int LOGN, bool FULL>
+// WIDE: this launch runs the wide output rows only, else the q-window rows (two launches over
+// the same chunk grid, so that each path gets the register budget of its own kernel: together
+// they spilled 52 bytes per lane, the q rows alone 16).
+template <int LOGN, bool FULL, bool WIDE>
 __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_c(CwtArgs a, const cpx* __restrict__ SB, const cpx* __restrict__ WB, const int* __restrict__ plan,
                 int K, float* __restrict__ coh) {
@@ -1277,9 +1318,9 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   const int ch = static_cast<int>(blk - b * a.nchunks);
   const int j0 = ch * a.chunk;
   const int j1 = min(a.S, j0 + a.chunk);
-  // any phase-C rows here?  (uniform: every thread reads the same plan entries)
+  // any rows of this launch's kind here?  (uniform: every thread reads the same plan entries)
   bool any = false;
-  for (int r = j0; r < j1; ++r) any |= (plan[r] & kPlanSpec) != 0;
+  for (int r = j0; r < j1; ++r) any |= (plan[r] & kPlanSpec) != 0 && (plan_eu(plan[r]) != 0) == WIDE;
   if (!any) return;
   cpx* my = lds + g * P::PADN;
   constexpr bool TWL = G::TWL;
@@ -1303,13 +1344,13 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     const int q = key(r0);
     int r1 = r0 + 1;
     while (r1 < nrow && key(r1) == q) ++r1;
-    if constexpr (P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
+    if constexpr (!WIDE && P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
       if (q == 1) wct_spec_rows<LOGN, 1, BUF, TWL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
       if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
         if (q == 2) wct_spec_rows<LOGN, 2, BUF, TWL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
       }
     }
-    if constexpr (LOGN >= kWideMinLogn) {
+    if constexpr (WIDE && LOGN >= kWideMinLogn) {
       if (q == 5) wct_wide_rows<LOGN, 1, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
       if (q == 6) wct_wide_rows<LOGN, 2, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
       if (q == 7) wct_wide_rows<LOGN, 3, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
@@ -1372,16 +1413,29 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
   if (a.n0 != (1 << LOGN)) {
-    hipLaunchKernelGGL((wct_phase_a<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
+    hipLaunchKernelGGL((wct_phase_a<LOGN, false, 0>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
                        plan);
-    return launch_status();
+    if ((rc = launch_status()) != kOk) return rc;
+    if (a.prune) {  // band rows exist only with pruning
+      hipLaunchKernelGGL((wct_phase_a<LOGN, false, 1>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
+                         plan);
+      rc = launch_status();
+    }
+    return rc;
   }
   // Full rows: the non-decimated rows' kernel, then (with decimated rows) their spectra and their
   // kernel.  (Running the first on a second stream beside the decimated work, and phase C beside
   // the decimated rows' kernel, measured a tie and 0.1 ms slower on C4: each saturates the CUs.)
-  hipLaunchKernelGGL((wct_phase_a<LOGN, true, false>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
+  hipLaunchKernelGGL((wct_phase_a<LOGN, true, 0>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
                      plan);
   if ((rc = launch_status()) != kOk) return rc;
+  // band rows that are not decimated: none when the decimation is on (a row of regime >= 1 has
+  // its CWT band within N/16, hence a decimation M <= N/8), so that launch is skipped then
+  if (a.prune && !dec) {
+    hipLaunchKernelGGL((wct_phase_a<LOGN, true, 1>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
+                       plan);
+    if ((rc = launch_status()) != kOk) return rc;
+  }
   if constexpr (LOGN >= kDecMinLogn) {
     if (dec) {
       for (int lm = kDecMaxLogm; lm >= kDecEngLogm; --lm) {
@@ -1398,7 +1452,7 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
       ad.chunk = ((wct_dec_rows_per_wg(a.batch) + rows - 1) / rows) * rows;
       if (ad.chunk > G::MAXCHUNK) ad.chunk = G::MAXCHUNK;
       ad.nchunks = (a.S + ad.chunk - 1) / ad.chunk;
-      hipLaunchKernelGGL((wct_phase_a<LOGN, true, true>), dim3(static_cast<unsigned>(a.batch * ad.nchunks)),
+      hipLaunchKernelGGL((wct_phase_a<LOGN, true, 2>), dim3(static_cast<unsigned>(a.batch * ad.nchunks)),
                          dim3(G::BLOCK), 0, st, ad, spec, TA, TB, SB, DY, WB, plan);
       return launch_status();
     }
@@ -1413,9 +1467,15 @@ static int launch_phase_c(const CwtArgs& a, const cpx* SB, const cpx* WB, const 
   using G = WctGeom<LOGN>;
   const dim3 gd(static_cast<unsigned>(a.batch * a.nchunks));
   if (a.n0 == (1 << LOGN))
-    hipLaunchKernelGGL((wct_phase_c<LOGN, true>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
+    hipLaunchKernelGGL((wct_phase_c<LOGN, true, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
   else
-    hipLaunchKernelGGL((wct_phase_c<LOGN, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
+    hipLaunchKernelGGL((wct_phase_c<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
+  int rc = launch_status();
+  if (rc != kOk || LOGN < kWideMinLogn || a.prune < 1 || options().wct_wide < 1 || K > kWideMaxK) return rc;
+  if (a.n0 == (1 << LOGN))
+    hipLaunchKernelGGL((wct_phase_c<LOGN, true, true>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
+  else
+    hipLaunchKernelGGL((wct_phase_c<LOGN, false, true>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
   return launch_status();
 }
 

@@ -38,31 +38,66 @@ __device__ __forceinline__ double u01(unsigned a, unsigned b) {  // (0, 1), 53 b
 
 // K10: AR(1) red noise, pycwt helpers.rednoise(N, g, a=1):
 //   y = lfilter([1, 0], [1, -g], randn(N + tau))[tau:], tau = ceil(-2 / ln|g|).
-// One thread per series (the recurrence is sequential; N <= 16384 keeps this in the
-// tens of microseconds).  Normals from Box-Muller on Philox words, fp64 recurrence.
-__global__ void __launch_bounds__(64) rednoise_kernel(float* __restrict__ out, long long ld,
-                                                      long long count, int n, double g, int tau,
-                                                      unsigned long long seed,
-                                                      unsigned long long first) {
-  const long long c = blockIdx.x * 64ll + threadIdx.x;
-  if (c >= count) return;
+// Normal i of series sid comes from Philox block (i / 2, sid) by Box-Muller (fp64).  One
+// workgroup per series; the recurrence y_i = g y_{i-1} + e_i is split into 256 chunks of L
+// consecutive samples: pass 1 runs each chunk from a zero state (its end value a_c), one
+// thread chains the chunks' carries (carry_c = g^L carry_{c-1} + a_{c-1}), pass 2 reruns each
+// chunk from its carry -- regenerating the same normals -- and writes y.  The sequential
+// recurrence of one thread per series took milliseconds per launch (N + tau ~ 8000 steps of
+// Philox + fp64 log / sincospi each); this is the same linear recurrence in a different
+// summation order (fp64, rounded to fp32 on store).
+__device__ __forceinline__ void rn_normals(unsigned long long sid, uint2 key, int i0, double (&e)[2]) {
+  const uint4 w = Philox::gen(make_uint4(static_cast<unsigned>(i0 >> 1), static_cast<unsigned>(sid),
+                                         static_cast<unsigned>(sid >> 32), 0x5eed5u), key);
+  const double r = sqrt(-2.0 * log(u01(w.x, w.y)));
+  double s, co;
+  sincospi(2.0 * u01(w.z, w.w), &s, &co);
+  e[0] = r * co;
+  e[1] = r * s;
+}
+
+constexpr int kRnThreads = 256;
+
+__global__ void __launch_bounds__(kRnThreads) rednoise_kernel(float* __restrict__ out, long long ld,
+                                                              long long count, int n, double g, int tau,
+                                                              unsigned long long seed,
+                                                              unsigned long long first) {
+  __shared__ double carry[kRnThreads];
+  const long long c = blockIdx.x;
   const unsigned long long sid = first + static_cast<unsigned long long>(c);
   const uint2 key = make_uint2(static_cast<unsigned>(seed), static_cast<unsigned>(seed >> 32));
   float* row = out + c * ld;
-  double y = 0.0;
   const int total = n + tau;
-  for (int i0 = 0; i0 < total; i0 += 2) {
-    // one Philox block -> two normals
-    const uint4 w = Philox::gen(make_uint4(static_cast<unsigned>(i0 >> 1), static_cast<unsigned>(sid),
-                                           static_cast<unsigned>(sid >> 32), 0x5eed5u), key);
-    const double r = sqrt(-2.0 * log(u01(w.x, w.y)));
-    double s, co;
-    sincospi(2.0 * u01(w.z, w.w), &s, &co);
-    const double e[2] = {r * co, r * s};
+  const int L = (((total + kRnThreads - 1) / kRnThreads) + 1) & ~1;  // even: chunks start on a block
+  const int t = threadIdx.x;
+  const int ib = min(total, t * L), ie = min(total, ib + L);
+  double y = 0.0;
+  for (int i0 = ib; i0 < ie; i0 += 2) {  // pass 1: the chunk from a zero state
+    double e[2];
+    rn_normals(sid, key, i0, e);
+    y = fma(g, y, e[0]);
+    if (i0 + 1 < ie) y = fma(g, y, e[1]);
+  }
+  carry[t] = y;
+  __syncthreads();
+  if (t == 0) {  // carry into chunk k = state after chunks 0..k-1
+    const double gl = pow(g, static_cast<double>(L));
+    double st = 0.0;
+    for (int k = 0; k < kRnThreads; ++k) {
+      const double a = carry[k];
+      carry[k] = st;
+      st = fma(gl, st, a);
+    }
+  }
+  __syncthreads();
+  y = carry[t];
+  for (int i0 = ib; i0 < ie; i0 += 2) {  // pass 2: from the carry, writing the samples >= tau
+    double e[2];
+    rn_normals(sid, key, i0, e);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int i = i0 + q;
-      if (i < total) {
+      if (i < ie) {
         y = fma(g, y, e[q]);
         if (i >= tau) row[i - tau] = static_cast<float>(y);
       }
@@ -119,9 +154,8 @@ extern "C" int wtmi_rednoise(float* out, long long ld, long long count, long lon
     if (tt > (1 << 26)) return kErrUnsupported;
     tau = static_cast<int>(tt);
   }
-  const long long blocks = (count + 63) / 64;
-  if (blocks > 0x7fffffffll) return kErrUnsupported;
-  hipLaunchKernelGGL(rednoise_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64), 0,
+  if (count > 0x7fffffffll) return kErrUnsupported;
+  hipLaunchKernelGGL(rednoise_kernel, dim3(static_cast<unsigned>(count)), dim3(kRnThreads), 0,
                      static_cast<hipStream_t>(stream), out, ld, count, static_cast<int>(n), g, tau, seed,
                      first_series);
   return launch_status();

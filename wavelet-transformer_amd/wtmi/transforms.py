@@ -393,7 +393,7 @@ def sig_cache_store(key, sig95) -> None:
 
 def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="morlet",
                      mc_count=300, progress=True, cache=True, seed=None, nbins=1000,
-                     max_pairs_per_launch=128):
+                     max_pairs_per_launch=512):
     """pycwt ``wct_significance`` on the GPU: mc_count passes of two AR(1) red-noise
     series (al1, al2), their coherence, and the per-scale counter of floor(R2 * nbins)
     outside the COI, batched max_pairs_per_launch passes per launch.  ``cache`` keeps
@@ -414,10 +414,11 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     if N > ops.MAX_SAMPLES:
         raise ValueError(f"wct_significance: noise length {N} exceeds the engine's "
                          f"{ops.MAX_SAMPLES} samples per row")
-    # pairs per launch: the smoothed-row workspace is 16 B per (pair, scale, sample); keep a
-    # launch's workspace near 4 GiB for long noise rows
+    # pairs per launch: all passes in one launch while the workspace (about 24 B per pair,
+    # scale and sample) stays under 8 GiB -- the app's 300 passes of ~8k-sample noise take
+    # one; long noise rows are split into several launches
     per_pair = max(1, ops.wct_workspace_bytes(1, N, sj.size))
-    max_pairs_per_launch = int(max(1, min(max_pairs_per_launch, (4 << 30) // per_pair)))
+    max_pairs_per_launch = int(max(1, min(max_pairs_per_launch, (8 << 30) // per_pair)))
     if seed is None:
         seed = int(np.random.SeedSequence().entropy) & ((1 << 64) - 1)
     dev = device()
