@@ -332,9 +332,9 @@ class C4(Workload):
     """XWT + WCT: 512 pairs x 8192, dj = 1/8 -> 97 scales."""
     name, axis, seed = "c4", "pair", 1004
     B, n, dj = 512, 8192, 1 / 8
-    kernel = ("moments<float> x2 + wct_spectra<13> + wct_plan<13> + wct_phase_a<13,full-band rows> (side stream) || "
-              "wct_dec_kernel<13,5..12> + wct_phase_a<13,decimated rows> + wct_phase_c<13>; "
-              "wct_phase_b<10>")
+    kernel = ("moments<float> x2 + wct_spectra<13> + wct_plan<13> + wct_phase_a<13,full-band rows> + "
+              "wct_dec_kernel<13,8..12> + wct_phase_a<13,decimated rows> + wct_wide_boxcar<10> + "
+              "wct_phase_c<13,q windows> + wct_phase_c<13,wide windows> + wct_phase_b<10>, one stream")
 
     def setup(self):
         from wtmi import transforms
@@ -403,6 +403,21 @@ CHECK_NAME = {"c2": "rank0_first_last_series_max_row_rel_err_vs_oracle",
               "c3": "rank0_round_trip_max_err_rel_to_max_x",
               "c4": "rank0_first_last_pair_coherence_max_abs_err_vs_oracle",
               "stub": "rank0_sum"}
+
+
+def kernel_roofline(cfg):
+    """Per-kernel roofline of the config from the newest committed profile
+    (profiles/rNN/kernel_roofline.json, scripts/kernel_roofline.py): each kernel's duration
+    (rocprofv3 trace of the timed steps), HBM bytes (PMC) and VALU issue share (PMC), and the
+    resource that binds it."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_roofline.json")), reverse=True):
+        with open(path) as fh:
+            ent = json.load(fh).get(cfg)
+        if ent:
+            keep = ("kernel", "ms", "bound", "frac", "hbm_GBps", "hbm_frac", "valu_busy")
+            return [{k: r[k] for k in keep} for r in ent["kernels"]], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def pmc_traffic(cfg, per_step):
@@ -613,6 +628,7 @@ def main():
     if rank == 0:
         achieved = wl.bytes / (kern_ms * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(args.config, wl.per_step)
+        per_kernel, ksrc = kernel_roofline(args.config)
         cfg = wl.config()
         cfg.update(wl.shard_config(world, args.scaling))
         if world > 1:
@@ -640,7 +656,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": tsrc, "scope": "rank 0's launches",
                          "kernel": wl.kernel, "kernel_ms": kern_ms,
-                         "algorithmic_bytes_per_launch": wl.bytes, "bytes_model": wl.bytes_note},
+                         "algorithmic_bytes_per_launch": wl.bytes, "bytes_model": wl.bytes_note,
+                         "per_kernel": per_kernel, "per_kernel_source": ksrc},
             "cpu_baseline": cpu,
             "check": {CHECK_NAME[args.config]: check},
         }

@@ -57,12 +57,15 @@ __device__ __forceinline__ float fast_atan2f(float y, float x) {
 // 16-position-per-thread row store needs one offset VGPR instead of 16 64-bit address
 // pairs (which the FFT kernels otherwise keep live across the scale loop).  The
 // pointer must be wave-uniform; readfirstlane makes that provable to the compiler.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+// bytes: the descriptor's extent; accesses past it are dropped (stores) or read 0 (loads) by
+// the hardware range check -- a padded row (n0 < N) passes n0 * sizeof(T) and stores its 16
+// positions per thread without per-lane branches.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes = 0x7fffffff) {
   const unsigned long long u = reinterpret_cast<unsigned long long>(p);
   const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(u));
   const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(u >> 32));
   void* q = reinterpret_cast<void*>((static_cast<unsigned long long>(hi) << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(q, 0, 0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {

@@ -28,17 +28,19 @@ __device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, 
   float* ps_ = (KIND & kOutSig) ? a.out_sig + rowbase : nullptr;
   float* pu_ = (KIND & kOutUV) ? a.out_u + rowbase : nullptr;
   float* pv_ = (KIND & kOutUV) ? a.out_v + rowbase : nullptr;
-  // Full rows whose owner is a whole wave (NT >= 64 -> the row, hence rowbase, is
-  // wave-uniform) go through buffer stores: SGPR row base + one voffset VGPR.
+  // Rows whose owner is a whole wave (NT >= 64 -> the row, hence rowbase, is wave-uniform)
+  // go through buffer stores: SGPR row base + one voffset VGPR; a padded row's positions
+  // past n0 fall outside the descriptor's extent and are dropped by the hardware.
   constexpr bool kBuf = P::NT >= kWave;
-  if constexpr (FULL && kBuf) {
+  if constexpr (kBuf) {
     __amdgpu_buffer_rsrc_t rw, rp, rs, ru, rv;
-    if constexpr (KIND & kOutW) rw = uniform_rsrc(pw_);
-    if constexpr (KIND & kOutPow) rp = uniform_rsrc(pp_);
-    if constexpr (KIND & kOutSig) rs = uniform_rsrc(ps_);
+    const int n8 = 8 * a.n0, n4 = 4 * a.n0;
+    if constexpr (KIND & kOutW) rw = uniform_rsrc(pw_, n8);
+    if constexpr (KIND & kOutPow) rp = uniform_rsrc(pp_, n4);
+    if constexpr (KIND & kOutSig) rs = uniform_rsrc(ps_, n4);
     if constexpr (KIND & kOutUV) {
-      ru = uniform_rsrc(pu_);
-      rv = uniform_rsrc(pv_);
+      ru = uniform_rsrc(pu_, n4);
+      rv = uniform_rsrc(pv_, n4);
     }
 #pragma unroll
     for (int m = 0; m < 16; ++m)

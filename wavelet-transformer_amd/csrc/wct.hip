@@ -111,14 +111,15 @@ __device__ __forceinline__ void load_spec(cpx (&X)[16], const cpx* row, int t) {
   load_spec_nz<LOGN, 16>(X, row, t);
 }
 
-// Row store of 16 positions per thread.  BUF (full rows owned by whole waves): buffer
-// stores off a wave-uniform row base, no per-position address registers; otherwise
-// plain stores masked to pos < n0.
+// Row store of 16 positions per thread.  BUF (rows owned by whole waves): buffer stores off
+// a wave-uniform row base, no per-position address registers, the descriptor's extent
+// n0 * sizeof(T) dropping the positions past a padded row's end; otherwise plain stores
+// masked to pos < n0.
 template <int LOGN, bool BUF, typename T, typename F>
 __device__ __forceinline__ void put_row(T* row, int t, int n0, F&& val) {
   using P = FftPlan<LOGN>;
   if constexpr (BUF) {
-    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row);
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row, n0 * static_cast<int>(sizeof(T)));
 #pragma unroll
     for (int m = 0; m < 16; ++m) buf_st(val(m), r, static_cast<int>(sizeof(T)) * t, static_cast<int>(sizeof(T)) * m * P::NT);
   } else {
@@ -585,7 +586,7 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
                                          const cpx* tw, int g, int t, int& par, const float4* twl) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  constexpr bool BUF = FULL && P::NT >= kWave;
+  constexpr bool BUF = P::NT >= kWave;  // padded rows too: put_row's extent
   const float f0 = static_cast<float>(a.f0);
   const int n0 = a.n0;
   for (int r = r0; r < r1; r += G::ROWS) {
@@ -1306,7 +1307,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
                 int K, float* __restrict__ coh) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  constexpr bool BUF = FULL && P::NT >= kWave;
+  constexpr bool BUF = P::NT >= kWave;  // padded rows too: put_row's extent
   __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::TWL_F4];
   cpx* lds = reinterpret_cast<cpx*>(lds4);
   float4* twl = lds4 + (G::ROWS * P::PADN) / 2;

@@ -292,29 +292,46 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
 
 
 # ------------------------------------------------------ WCT Monte-Carlo significance
+_GEOM_CACHE: dict = {}
+
+
 def wct_sig_geometry(dt, dj, s0, J, wavelet="morlet"):
     """pycwt wct_significance set-up: noise length N = ceil(6 s0 2^(J dj) / dt), scales,
     and per scale the interval [t_lo, t_hi) of points outside the cone of influence
     (period_s <= coi_t; the COI is a triangle, so the set is an interval);
-    maxscale = last scale with any such point (the counter runs over s < maxscale)."""
+    maxscale = last scale with any such point (the counter runs over s < maxscale).
+    The COI rises over the first half of the row, so each interval's ends come from one
+    binary search on that half with the very comparison pycwt makes (period <= coi);
+    results are kept per argument set (the app repeats its settings)."""
     wavelet = as_morlet(wavelet)
+    key = (float(dt), float(dj), float(s0), int(J), wavelet.f0)
+    hit = _GEOM_CACHE.get(key)
+    if hit is not None:
+        return hit[0], hit[1].copy(), hit[2].copy(), hit[3].copy(), hit[4].copy(), hit[5]
     ms = s0 * (2 ** (J * dj)) / dt
     N = int(np.ceil(ms * 6))
     sj = s0 * 2 ** (np.arange(0, J + 1) * dj)
     period = wavelet.flambda() * sj
     coi = cone_of_influence(N, dt, wavelet)
-    t_lo = np.zeros(J + 1, dtype=np.int32)
-    t_hi = np.zeros(J + 1, dtype=np.int32)
-    anyout = np.zeros(J + 1, dtype=bool)
+    half = (N + 1) // 2  # coi[:half] is non-decreasing, coi[t] == coi[N - 1 - t]
+    rise = np.maximum.accumulate(coi[:half])
+    first = np.searchsorted(rise, period, side="left")  # first t with coi[t] >= period
+    # pycwt's own comparison decides the boundary samples (rounding of the triangle)
     for s in range(J + 1):
-        idx = np.nonzero(period[s] <= coi)[0]
-        if idx.size:
-            t_lo[s], t_hi[s] = idx[0], idx[-1] + 1
-            anyout[s] = True
+        t = int(first[s])
+        while t > 0 and period[s] <= coi[t - 1]:
+            t -= 1
+        while t < half and not (period[s] <= coi[t]):
+            t += 1
+        first[s] = t
+    anyout = first < half
+    t_lo = np.where(anyout, first, 0).astype(np.int32)
+    t_hi = np.where(anyout, N - first, 0).astype(np.int32)
     if not anyout.any():
         raise ValueError("no scale has points outside the cone of influence")
     maxscale = int(np.nonzero(anyout)[0][-1])
-    return N, sj, t_lo, t_hi, anyout, maxscale
+    _GEOM_CACHE[key] = (N, sj, t_lo, t_hi, anyout, maxscale)
+    return N, sj.copy(), t_lo.copy(), t_hi.copy(), anyout.copy(), maxscale
 
 
 def significance_from_histogram(wlc: np.ndarray, anyout: np.ndarray, maxscale: int,
@@ -326,14 +343,35 @@ def significance_from_histogram(wlc: np.ndarray, anyout: np.ndarray, maxscale: i
     nbins = wlc.shape[1]
     sig95 = np.zeros(anyout.size)
     sig95[anyout] = np.nan
+    if maxscale < 1:
+        return sig95
     r2y = (np.arange(nbins) + 0.5) / nbins
-    for s in range(maxscale):
-        sel = wlc[s] != 0
-        if not sel.any():
-            continue
-        P = np.cumsum(wlc[s, sel])
-        P = (P - 0.5) / P[-1]
-        sig95[s] = np.interp(significance_level, P, r2y[sel])
+    # all scales at once: np.interp over each scale's non-empty bins, i.e. the first
+    # non-empty bin whose P reaches the level and the non-empty bin before it
+    w = np.asarray(wlc[:maxscale], dtype=np.float64)
+    nz = w != 0
+    cum = np.cumsum(w, axis=1)
+    tot = cum[:, -1:]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        P = (cum - 0.5) / tot
+    reach = nz & (P >= significance_level)
+    hi = np.where(reach.any(axis=1), reach.argmax(axis=1), nbins - 1)
+    idx = np.where(nz, np.arange(nbins), -1)
+    prev = np.maximum.accumulate(idx, axis=1)  # last non-empty bin at or before each bin
+    rows = np.arange(maxscale)
+    has = reach.any(axis=1)
+    lastnz = prev[:, -1]
+    lo = np.where(hi > 0, prev[rows, np.maximum(hi - 1, 0)], -1)
+    h = np.where(has, hi, np.maximum(lastnz, 0))
+    lo_c = np.maximum(lo, 0)
+    p0, p1 = P[rows, lo_c], P[rows, h]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        lin = r2y[lo_c] + (significance_level - p0) * (r2y[h] - r2y[lo_c]) / (p1 - p0)
+    # np.interp clamps outside the points: below the first non-empty bin -> its value, above
+    # the last -> the last's; a scale with no counts keeps pycwt's initial value
+    out = np.where(has & (lo >= 0), lin, r2y[h])
+    out = np.where(lastnz < 0, sig95[:maxscale], out)
+    sig95[:maxscale] = out
     return sig95
 
 
