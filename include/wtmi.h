@@ -93,6 +93,15 @@ int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long ba
                     float* out_coh, float* out_power, float* out_phase, float* out_u,
                     float* out_v, void* stream);
 
+/* wtmi_wct_morlet with pycwt's own normalisation of both series, (y - mean) / std with the
+ * moments in fp64 over each series (pycwt.wct / xwt normalize=True, src/wct.py:106-118), done
+ * inside the transform's first kernel -- no separate moments / affine launches.  Rows of
+ * 9 .. 16384 samples (-2 otherwise: normalise through wtmi_series_affine + affine1/2).    */
+int wtmi_wct_morlet_norm(const float* x1, const float* x2, long long ld, long long batch,
+                         long long n0, const double* scales, int n_scales, double dt, double f0,
+                         int boxcar, void* workspace, float* out_coh, float* out_power,
+                         float* out_phase, float* out_u, float* out_v, void* stream);
+
 /* ---- WCT Monte-Carlo significance (K10 / K11) ---------------------------------
  * Replace the pieces of pycwt.wct_significance reached from src/wct.py:106-118 with
  * sig=True.
@@ -104,12 +113,18 @@ int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long ba
  *   clamp(floor(coh[p][s][t] * nbins), 0, nbins-1) over all pairs p and
  *   t in [t_lo[s], t_hi[s]) (the points outside the cone of influence; t_lo/t_hi are
  *   device int arrays) into hist[n_hist_scales][nbins] (uint32, caller-zeroed).
- *   nbins <= 4096.                                                                  */
+ *   nbins <= 4096.
+ * wtmi_coherence_quantile: the quantile step of wct_significance for the first n_scales
+ *   rows of hist[.][nbins]: out[s] = np.interp(level, P, (bin + 1/2) / nbins) over the
+ *   non-empty bins, P = (cumsum - 1/2) / total (0 for a row without counts); out is a device
+ *   float64 [n_scales].                                                              */
 int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g,
                   unsigned long long seed, unsigned long long first_series, void* stream);
 int wtmi_coherence_histogram(const float* coh, long long batch, long long n0, int n_scales,
                              const int* t_lo, const int* t_hi, int n_hist_scales, int nbins,
                              unsigned int* hist, void* stream);
+int wtmi_coherence_quantile(const unsigned int* hist, int n_scales, int nbins, double level, double* out,
+                            void* stream);
 
 /* ---- MODWT (K3 / K4) -----------------------------------------------------------
  * Replace src/modwt.py:126-144 (modwt: rows [W_1..W_J, V_J]) and :147-160 (imodwt).

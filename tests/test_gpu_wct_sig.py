@@ -91,3 +91,25 @@ def test_run_wct_with_significance_app_shape():
     fin = np.isfinite(res.significance_levels)
     assert fin.mean() > 0.5  # NaN only on the scales pycwt leaves NaN
     assert (res.significance_levels[fin] > 0).all()
+
+
+def test_device_quantile_matches_host_rule():
+    """wtmi_coherence_quantile (the quantile step on the device) == the host restatement
+    significance_from_histogram (pycwt's rule over the non-empty bins) on random counters,
+    including empty scales, single-bin scales and levels below / above every P."""
+    import torch
+    from wtmi import ops, transforms
+    rng = np.random.default_rng(5)
+    for trial in range(40):
+        S, nb = int(rng.integers(1, 60)), int(rng.choice([7, 100, 1000, 4096]))
+        w = (rng.integers(0, 6, (S, nb)) * (rng.random((S, nb)) < rng.random())).astype(np.int64)
+        if trial % 4 == 0:
+            w[rng.integers(0, S)] = 0
+        if trial % 5 == 0:
+            w[:] = 0
+            w[:, rng.integers(0, nb)] = rng.integers(1, 9)
+        level = float(rng.choice([0.95, 0.5, 0.001, 0.9999]))
+        dev = torch.tensor(w.astype(np.uint32).view(np.int32), device="cuda")
+        got = ops.coherence_quantile(dev, S, level).cpu().numpy()
+        ref = transforms.significance_from_histogram(w.astype(np.float64), np.zeros(S, bool), S, level)
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-15, err_msg=f"trial {trial}")

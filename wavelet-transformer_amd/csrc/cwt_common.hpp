@@ -35,6 +35,8 @@ struct CwtArgs {
   float mA, mB, mP, mcre, mcim;
   int mgate;
   double mlnorm;         // log2 of the mother's normalisation (Morlet: log2 pi^-1/4)
+  int norm;              // WCT: normalise each series in the load, (y - mean) / std (pycwt
+                         // xwt / wct), in place of the affine pointers
 };
 
 // Filter constants of a mother wavelet (pycwt 0.4.0b0 mothers.py: Paul.psi_ft, DOG.psi_ft).
@@ -150,6 +152,50 @@ __device__ __forceinline__ float demean_row(cpx (&v)[16], int n0, int t, float* 
   for (int m = 0; m < 16; ++m)
     if (t + m * P::NT < n0) v[m].x -= mu;
   return mu;
+}
+
+// pycwt's wct / xwt normalisation inside the load: y' = (y - mean) / std (ddof 0) with the
+// moments in fp64 over the row's n0 samples (two passes over the registers: mean, then the
+// centred sum of squares), applied in fp64 and rounded once to fp32 -- what the separate
+// moments + affine launches (wtmi_series_affine, mode normalise) computed.  redd: >= BLOCK/64
+// doubles of LDS; every thread of the workgroup must call this.
+template <int LOGN>
+__device__ __forceinline__ double row_sum_f64(double s, int t, double* redd) {
+  using P = FftPlan<LOGN>;
+  constexpr int W = P::NT < kWave ? P::NT : kWave;
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) s += __shfl_xor(s, o, W);
+  if constexpr (P::NT > kWave) {
+    constexpr int WPR = P::NT / kWave;
+    const int wv = threadIdx.x / kWave;
+    __syncthreads();  // redd reuse
+    if ((threadIdx.x & (kWave - 1)) == 0) redd[wv] = s;
+    __syncthreads();
+    const int w0 = wv & ~(WPR - 1);
+    s = 0.0;
+#pragma unroll
+    for (int w = 0; w < WPR; ++w) s += redd[w0 + w];
+  }
+  return s;
+}
+
+template <int LOGN>
+__device__ __forceinline__ void normalize_row(cpx (&v)[16], int n0, int t, double* redd) {
+  using P = FftPlan<LOGN>;
+  double s = 0.0;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) s += static_cast<double>(v[m].x);  // padding entries are zero
+  const double mu = row_sum_f64<LOGN>(s, t, redd) / n0;
+  double q = 0.0;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const double d = t + m * P::NT < n0 ? static_cast<double>(v[m].x) - mu : 0.0;
+    q = fma(d, d, q);
+  }
+  const double inv = 1.0 / sqrt(row_sum_f64<LOGN>(q, t, redd) / n0);
+#pragma unroll
+  for (int m = 0; m < 16; ++m)
+    if (t + m * P::NT < n0) v[m].x = static_cast<float>((static_cast<double>(v[m].x) - mu) * inv);
 }
 
 // X[k] += mu * D[k] for the 16 bins k = t + m*NT this thread holds (forward spectrum).

@@ -55,17 +55,18 @@ __device__ __forceinline__ void smooth_filter(cpx (&v)[16], float beta, float sc
   }
 }
 
-// Forward spectra of both series of every pair: spec[b][which][k], natural order.
+// Forward spectra of both series of every pair: spec[b][which][k], natural order (with
+// a.norm, of the normalised series).  Workgroup blk of wct_spectra_plan.
 template <int LOGN>
-__global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, cpx* __restrict__ spec) {
+__device__ __forceinline__ void spectra_body(const CwtArgs& a, cpx* __restrict__ spec, long long blk) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
   __shared__ cpx lds[G::ROWS * P::PADN];
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
   const int t = fft_thread<LOGN>(tid - g * P::NT);
-  // row group g handles series (pair, which) = blockIdx.x * ROWS + g
-  const long long item = static_cast<long long>(blockIdx.x) * G::ROWS + g;
+  // row group g handles series (pair, which) = blk * ROWS + g
+  const long long item = blk * G::ROWS + g;
   const bool valid = item < 2 * a.batch;
   const long long b = valid ? item >> 1 : 0;
   const int which = static_cast<int>(item & 1);
@@ -73,11 +74,13 @@ __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra(CwtArgs a, c
   fft_twiddles<LOGN>(tw, t);
   int par = 0;
   __shared__ float red[G::BLOCK / kWave];
+  __shared__ double redd[G::BLOCK / kWave];
   cpx X[16];
   if (which == 0)
-    load_series<LOGN>(X, a.x, a.affine, b, a.ld, a.n0, t);
+    load_series<LOGN>(X, a.x, a.norm ? nullptr : a.affine, b, a.ld, a.n0, t);
   else
-    load_series<LOGN>(X, a.x2, a.affine2, b, a.ld, a.n0, t);
+    load_series<LOGN>(X, a.x2, a.norm ? nullptr : a.affine2, b, a.ld, a.n0, t);
+  if (a.norm) normalize_row<LOGN>(X, a.n0, t, redd);
   const float mu = demean_row<LOGN>(X, a.n0, t, red);
   fft_row<LOGN, -1, 1>(X, lds + g * P::PADN, 0, tw, t, par);
   add_mean_spectrum<LOGN>(X, mu, a.n0, t);
@@ -328,10 +331,9 @@ __device__ __forceinline__ int plan_q(const double* scales, int r, double dt, do
 // scratch: 2 S ints (row regimes, then each output row's window regime or -1), then the
 // decimated rows' list (S ints) and schedule (kDecSched ints), see wct_dec_kernel.
 template <int LOGN>
-__global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict__ scales, int S, double dt,
-                                                       double f0, int K, int prune, int dec, int wide,
-                                                       long long batch, int* __restrict__ plan,
-                                                       int* __restrict__ scratch) {
+__device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales, int S, double dt, double f0,
+                                              int K, int prune, int dec, int wide, long long batch,
+                                              int* __restrict__ plan, int* __restrict__ scratch) {
   __shared__ int last;
   if (threadIdx.x == 0) last = -1;
   const int LO = K / 2, HI = (K - 1) / 2;
@@ -418,6 +420,18 @@ __global__ void __launch_bounds__(256) wct_plan_kernel(const double* __restrict_
     const int e = plan_dec(plan[r]);
     if (e > 0) rows[atomicAdd(&cur[max(LOGN - e, kDecEngLogm)], 1)] = r;
   }
+}
+
+// Spectra and plan in one launch: workgroups 0 .. gridDim - 2 transform the series, the last
+// one plans the rows (they are independent; one launch less on the dependent chain).
+template <int LOGN>
+__global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra_plan(CwtArgs a, cpx* __restrict__ spec,
+                                                                         int K, int dec, int wide,
+                                                                         int* __restrict__ plan) {
+  if (blockIdx.x + 1 == gridDim.x)
+    wct_plan_body<LOGN>(a.scales, a.S, a.dt, a.f0, K, a.prune, dec, wide, a.batch, plan, plan + a.S + 1);
+  else
+    spectra_body<LOGN>(a, spec, blockIdx.x);
 }
 
 struct WctRowCtx {
@@ -1373,19 +1387,37 @@ static int wct_dec_rows_per_wg(long long batch) {
   return o > 0 ? o : (batch <= 256 ? 2 : 4);
 }
 
+// Side stream of the calling thread on the current device (created once; thread_local, so
+// concurrent callers never share one): the full-band rows' kernel runs there beside the
+// decimated rows' chain (fork after the plan, join before the spectral boxcar).  A small batch
+// (one GPU's shard of a strong-scaling run) leaves CUs idle in each kernel; two independent
+// kernels in flight fill them.
+struct SideStream {
+  hipStream_t s = nullptr;
+  // fork: spectra + plan done (main); k0: full-band rows done (side); dec: decimated spectra
+  // done (main); join: the side stream's last kernel done
+  hipEvent_t fork = nullptr, k0 = nullptr, dec = nullptr, join = nullptr;
+};
+static SideStream* side_stream() {
+  constexpr int kMaxDev = 64;
+  thread_local SideStream tl[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  SideStream& ss = tl[dev];
+  if (!ss.s) {
+    if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return ss.s = nullptr, nullptr;
+    for (hipEvent_t* e : {&ss.fork, &ss.k0, &ss.dec, &ss.join})
+      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  return &ss;
+}
+
 template <int LOGN>
 static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY, cpx* WB, int* plan,
-                          int K, float* coh, hipStream_t st) {
+                          int K, float* coh, hipStream_t st, SideStream* side) {
   using G = WctGeom<LOGN>;
-  {
-    const long long items = 2 * a.batch;
-    const long long sgrid = (items + G::ROWS - 1) / G::ROWS;
-    if (sgrid > 0x7fffffffll) return kErrUnsupported;
-    hipLaunchKernelGGL(wct_spectra<LOGN>, dim3(static_cast<unsigned>(sgrid)), dim3(G::BLOCK), 0, st, a,
-                       spec);
-    const int rc = launch_status();
-    if (rc != kOk) return rc;
-  }
+  const long long sgrid = (2 * a.batch + G::ROWS - 1) / G::ROWS;  // spectra workgroups
+  if (sgrid + 1 > 0x7fffffffll) return kErrUnsupported;
   const int rows = G::ROWS;
   // Row costs differ a lot (full-band rows several transforms, band rows few): more,
   // shorter workgroups balance better.  C4 ms (one box, two alternations): target 2048
@@ -1408,8 +1440,8 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   if (grid > 0x7fffffffll || a.batch * a.S > 0x7fffffffll - 64) return kErrUnsupported;
   // decimated rows: full rows, pruning level 2, Morlet negative frequencies negligible
   const int dec = (a.prune >= 2 && a.n0 == (1 << LOGN) && LOGN >= kDecMinLogn && a.f0 >= kBandF0) ? 1 : 0;
-  hipLaunchKernelGGL(wct_plan_kernel<LOGN>, dim3(1), dim3(256), 0, st, a.scales, a.S, a.dt, a.f0, K,
-                     a.prune, dec, options().wct_wide, a.batch, plan, plan + a.S + 1);
+  hipLaunchKernelGGL(wct_spectra_plan<LOGN>, dim3(static_cast<unsigned>(sgrid + 1)), dim3(G::BLOCK), 0, st, a,
+                     spec, K, dec, options().wct_wide, plan);
   int rc = launch_status();
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
@@ -1424,12 +1456,18 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
     }
     return rc;
   }
-  // Full rows: the non-decimated rows' kernel, then (with decimated rows) their spectra and their
-  // kernel.  (Running the first on a second stream beside the decimated work, and phase C beside
-  // the decimated rows' kernel, measured a tie and 0.1 ms slower on C4: each saturates the CUs.)
-  hipLaunchKernelGGL((wct_phase_a<LOGN, true, 0>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
+  // Full rows: the full-band rows' kernel -- on the side stream when the caller passes one (the
+  // caller joins it) -- then the decimated rows' spectra and their kernel.
+  hipStream_t sa = st;
+  if (side) {
+    if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+      return launch_status();
+    sa = side->s;
+  }
+  hipLaunchKernelGGL((wct_phase_a<LOGN, true, 0>), gd, dim3(G::BLOCK), 0, sa, a, spec, TA, TB, SB, DY, WB,
                      plan);
   if ((rc = launch_status()) != kOk) return rc;
+  if (side && hipEventRecord(side->k0, side->s) != hipSuccess) return launch_status();
   // band rows that are not decimated: none when the decimation is on (a row of regime >= 1 has
   // its CWT band within N/16, hence a decimation M <= N/8), so that launch is skipped then
   if (a.prune && !dec) {
@@ -1448,6 +1486,7 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
         }
         if (rc != kOk) return rc;
       }
+      if (side && hipEventRecord(side->dec, st) != hipSuccess) return launch_status();
       // decimated rows cost one to three band inverses each: chunks of their own length
       CwtArgs ad = a;
       ad.chunk = ((wct_dec_rows_per_wg(a.batch) + rows - 1) / rows) * rows;
@@ -1707,11 +1746,10 @@ extern "C" long long wtmi_wct_workspace_bytes(long long batch, long long n0, int
          4ll * (4 * n_scales + 1 + kDecSched);
 }
 
-extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
-                               long long n0, const double* affine1, const double* affine2,
-                               const double* scales, int n_scales, double dt, double f0, int boxcar,
-                               void* workspace, float* out_coh, float* out_power, float* out_phase,
-                               float* out_u, float* out_v, void* stream) {
+static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long long batch, long long n0,
+                           const double* affine1, const double* affine2, int norm, const double* scales,
+                           int n_scales, double dt, double f0, int boxcar, void* workspace, float* out_coh,
+                           float* out_power, float* out_phase, float* out_u, float* out_v, void* stream) {
   if (!x1 || !x2 || !scales || !workspace || !out_coh || n0 < 0 || batch < 0 || n_scales < 0 ||
       ld < n0 || boxcar < 1)
     return kErrArg;
@@ -1735,6 +1773,8 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   a.out_v = out_v;
   a.out_pow = out_power;
   a.out_sig = out_phase;  // phase-angle plane (atan2 of W12)
+  a.norm = norm;
+  if (norm && (n0 > (1 << 14) || n0 <= 8)) return kErrUnsupported;  // in-load normalisation: FFT rows
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n0 > (1 << 14)) return wct_long(a, boxcar, workspace, out_coh, st);
   if (logn < 4) {  // n0 <= 8: below the FFT engine's minimum row
@@ -1761,8 +1801,14 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
   ws += wct_wb_bytes(batch, n0, n_scales);
   int* plan = reinterpret_cast<int*>(ws);
   int rc;
+  // side stream for the full-band rows beside the decimated chain (full rows with decimation:
+  // LOGN >= kDecMinLogn, n0 = N, pruning 2), option wct_side_stream
+  SideStream* side = nullptr;
+  if (options().wct_side_stream && logn >= kDecMinLogn && n0 == (1ll << logn) && options().wct_prune >= 2 &&
+      f0 >= kBandF0)
+    side = side_stream();
   switch (logn) {
-#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, WB, plan, boxcar, out_coh, st); break;
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, WB, plan, boxcar, out_coh, st, side); break;
     WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
     WTMI_A(12) WTMI_A(13) WTMI_A(14)
 #undef WTMI_A
@@ -1779,6 +1825,15 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
       default: return kErrUnsupported;
     }
   };
+  // With the side stream (full rows, decimation on): the spectral boxcar and phase C run there
+  // once the decimated spectra are done (they need the WB / SB spectra of the full-band rows,
+  // which the side stream made, and of the decimated rows), while phase B runs here once the
+  // full-band rows' time-domain rows are done; the caller's stream then joins the side stream.
+  hipStream_t sc = st;
+  if (side) {
+    if (hipStreamWaitEvent(side->s, side->dec, 0) != hipSuccess) return launch_status();
+    sc = side->s;
+  }
   // spectral boxcar of the wide windows (their sums over the output rows' WB slots)
   if (wct_wb_bytes(batch, n0, n_scales) > 0 && a.prune >= 1 && boxcar <= kWideMaxK) {
     const long long tiles = ((1ll << logn) / 2 + 255) / 256;
@@ -1786,7 +1841,7 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
     switch (boxcar) {
 #define WTMI_W(KK)                                                                                         \
   case KK:                                                                                                 \
-    hipLaunchKernelGGL(wct_wide_boxcar<KK>, dim3(static_cast<unsigned>(batch * tiles)), dim3(256), 0, st, WB, \
+    hipLaunchKernelGGL(wct_wide_boxcar<KK>, dim3(static_cast<unsigned>(batch * tiles)), dim3(256), 0, sc, WB, \
                        batch, 1 << logn, n_scales, plan);                                                 \
     break;
       WTMI_W(1) WTMI_W(2) WTMI_W(3) WTMI_W(4) WTMI_W(5) WTMI_W(6) WTMI_W(7) WTMI_W(8)
@@ -1797,8 +1852,30 @@ extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, l
     }
     if ((rc = launch_status()) != kOk) return rc;
   }
-  // (phase B on a side stream beside phase C, fork/join by events, measured no faster:
-  // C4 4.21-4.36 vs 4.23-4.24 ms -- phase C's workgroups hold the CUs, r02)
-  if ((rc = phase_c(st)) != kOk) return rc;
+  if ((rc = phase_c(sc)) != kOk) return rc;
+  if (side) {
+    if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->k0, 0) != hipSuccess)
+      return launch_status();
+    if ((rc = wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st)) != kOk) return rc;
+    if (hipStreamWaitEvent(st, side->join, 0) != hipSuccess) return launch_status();
+    return kOk;
+  }
   return wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st);
+}
+
+extern "C" int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long batch,
+                               long long n0, const double* affine1, const double* affine2,
+                               const double* scales, int n_scales, double dt, double f0, int boxcar,
+                               void* workspace, float* out_coh, float* out_power, float* out_phase,
+                               float* out_u, float* out_v, void* stream) {
+  return wct_morlet_impl(x1, x2, ld, batch, n0, affine1, affine2, 0, scales, n_scales, dt, f0, boxcar, workspace,
+                         out_coh, out_power, out_phase, out_u, out_v, stream);
+}
+
+extern "C" int wtmi_wct_morlet_norm(const float* x1, const float* x2, long long ld, long long batch,
+                                    long long n0, const double* scales, int n_scales, double dt, double f0,
+                                    int boxcar, void* workspace, float* out_coh, float* out_power,
+                                    float* out_phase, float* out_u, float* out_v, void* stream) {
+  return wct_morlet_impl(x1, x2, ld, batch, n0, nullptr, nullptr, 1, scales, n_scales, dt, f0, boxcar, workspace,
+                         out_coh, out_power, out_phase, out_u, out_v, stream);
 }

@@ -139,6 +139,80 @@ __global__ void __launch_bounds__(kHistThreads) coherence_hist_kernel(
     if (h[i]) atomicAdd(&hist[static_cast<long long>(s) * nbins + i], h[i]);
 }
 
+// K15: the quantile step of pycwt's wct_significance on the device: for each scale s <
+// maxscale, P = (cumsum(counts over the non-empty bins) - 1/2) / total and the level is
+// np.interp(level, P, (bin + 1/2) / nbins) over those bins (clamped at both ends; a scale
+// without counts keeps 0).  One workgroup per scale: an exact 64-bit integer prefix sum over
+// the bins, the first non-empty bin whose P reaches the level and the non-empty bin before it
+// (LDS min / max), then one thread interpolates in fp64.  Only the [maxscale] levels travel
+// to the host instead of the [maxscale][nbins] counter.
+constexpr int kQThreads = 256;
+
+__global__ void __launch_bounds__(kQThreads) coherence_quantile_kernel(const unsigned* __restrict__ hist,
+                                                                       int nbins, double level,
+                                                                       double* __restrict__ out) {
+  __shared__ unsigned long long part[kQThreads];
+  __shared__ int s_hi, s_lo, s_last;
+  const int s = blockIdx.x, t = threadIdx.x;
+  const unsigned* h = hist + static_cast<long long>(s) * nbins;
+  const int per = (nbins + kQThreads - 1) / kQThreads;
+  const int b0 = min(nbins, t * per), b1 = min(nbins, b0 + per);
+  unsigned long long acc = 0;
+  for (int i = b0; i < b1; ++i) acc += h[i];
+  part[t] = acc;
+  if (t == 0) {
+    s_hi = nbins;
+    s_lo = -1;
+    s_last = -1;
+  }
+  __syncthreads();
+  for (int o = 1; o < kQThreads; o <<= 1) {  // inclusive scan of the per-thread sums
+    const unsigned long long v = t >= o ? part[t - o] : 0ull;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const unsigned long long tot = part[kQThreads - 1];
+  unsigned long long c = t > 0 ? part[t - 1] : 0ull;
+  int first = nbins, last = -1;
+  for (int i = b0; i < b1; ++i) {
+    if (!h[i]) continue;
+    c += h[i];
+    last = i;
+    if (first == nbins && (static_cast<double>(c) - 0.5) / static_cast<double>(tot) >= level) first = i;
+  }
+  if (first < nbins) atomicMin(&s_hi, first);
+  if (last >= 0) atomicMax(&s_last, last);
+  __syncthreads();
+  const int hi = s_hi;
+  for (int i = b0; i < b1 && i < hi; ++i)  // the last non-empty bin before hi
+    if (h[i]) atomicMax(&s_lo, i);
+  __syncthreads();
+  if (t != 0) return;
+  const double nb = static_cast<double>(nbins);
+  if (s_last < 0) {  // no counts at all: the level stays 0
+    out[s] = 0.0;
+    return;
+  }
+  if (hi == nbins) {  // the level lies above every P: np.interp clamps to the last point
+    out[s] = (s_last + 0.5) / nb;
+    return;
+  }
+  if (s_lo < 0) {  // at or below the first point: its value
+    out[s] = (hi + 0.5) / nb;
+    return;
+  }
+  unsigned long long clo = 0, chi = 0;  // cumulative counts through lo and hi
+  for (int i = 0; i <= hi; ++i) {
+    chi += h[i];
+    if (i == s_lo) clo = chi;
+  }
+  const double td = static_cast<double>(tot);
+  const double p0 = (static_cast<double>(clo) - 0.5) / td, p1 = (static_cast<double>(chi) - 0.5) / td;
+  const double y0 = (s_lo + 0.5) / nb, y1 = (hi + 0.5) / nb;
+  out[s] = y0 + (level - p0) * (y1 - y0) / (p1 - p0);
+}
+
 }  // namespace wtmi
 
 using namespace wtmi;
@@ -178,5 +252,14 @@ extern "C" int wtmi_coherence_histogram(const float* coh, long long batch, long 
   hipLaunchKernelGGL(coherence_hist_kernel, dim3(static_cast<unsigned>(grid)), dim3(kHistThreads), 0,
                      static_cast<hipStream_t>(stream), coh, batch, n0, n_scales, t_lo, t_hi, nbins,
                      static_cast<int>(parts), hist);
+  return launch_status();
+}
+
+extern "C" int wtmi_coherence_quantile(const unsigned int* hist, int n_scales, int nbins, double level,
+                                       double* out, void* stream) {
+  if (!hist || !out || n_scales < 0 || nbins < 1 || !(level >= 0.0 && level <= 1.0)) return kErrArg;
+  if (n_scales == 0) return kOk;
+  hipLaunchKernelGGL(coherence_quantile_kernel, dim3(static_cast<unsigned>(n_scales)), dim3(kQThreads), 0,
+                     static_cast<hipStream_t>(stream), hist, nbins, level, out);
   return launch_status();
 }

@@ -310,9 +310,11 @@ def wct_workspace_bytes(batch: int, n0: int, n_scales: int) -> int:
 def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
                boxcar: int, affine1=None, affine2=None, want_uv: bool = True,
                want_power: bool = False, want_phase: bool = False,
-               workspace: Optional[torch.Tensor] = None):
+               workspace: Optional[torch.Tensor] = None, normalize: bool = False):
     """Wavelet coherence of row pairs; returns dict coh [B,S,n0] (+ u, v, power =
-    |W1 W2*|^2, phase = angle(W1 W2*))."""
+    |W1 W2*|^2, phase = angle(W1 W2*)).  normalize: pycwt's (y - mean) / std of each series,
+    done inside the transform (wtmi_wct_morlet_norm; rows of 9..16384 samples, affine must
+    then be None)."""
     x1, x2 = _pair_rows(x1, x2)
     B, n0 = x1.shape
     S = _n_scales(scales)
@@ -341,11 +343,19 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
         res["u"] = torch.empty(shape, dtype=torch.float32, device=dev)
         res["v"] = torch.empty(shape, dtype=torch.float32, device=dev)
     a1, a2 = _f64_arg(affine1, dev), _f64_arg(affine2, dev)
+    if normalize and (a1 is not None or a2 is not None or not 8 < n0 <= 16384):
+        raise ValueError("normalize=True: rows of 9..16384 samples and no affine coefficients")
     with torch.cuda.device(dev):
-        _lib.call("wtmi_wct_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
-                  _ptr(sc), S, float(dt), float(f0), int(boxcar), _ptr(workspace),
-                  _ptr(res["coh"]), _ptr(res.get("power")), _ptr(res.get("phase")),
-                  _ptr(res.get("u")), _ptr(res.get("v")), _stream(dev))
+        if normalize:
+            _lib.call("wtmi_wct_morlet_norm", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(sc), S,
+                      float(dt), float(f0), int(boxcar), _ptr(workspace), _ptr(res["coh"]),
+                      _ptr(res.get("power")), _ptr(res.get("phase")), _ptr(res.get("u")),
+                      _ptr(res.get("v")), _stream(dev))
+        else:
+            _lib.call("wtmi_wct_morlet", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, _ptr(a1), _ptr(a2),
+                      _ptr(sc), S, float(dt), float(f0), int(boxcar), _ptr(workspace),
+                      _ptr(res["coh"]), _ptr(res.get("power")), _ptr(res.get("phase")),
+                      _ptr(res.get("u")), _ptr(res.get("v")), _stream(dev))
     return res
 
 
@@ -384,6 +394,20 @@ def coherence_histogram(coh: torch.Tensor, t_lo: torch.Tensor, t_hi: torch.Tenso
         _lib.call("wtmi_coherence_histogram", _ptr(coh), B, n0, S, _ptr(lo), _ptr(hi),
                   int(n_hist_scales), int(nbins), _ptr(hist), _stream(dev))
     return hist
+
+
+def coherence_quantile(hist: torch.Tensor, n_scales: int, level: float) -> torch.Tensor:
+    """Per-scale level of the Monte-Carlo counter hist [>= n_scales, nbins] (int32 view of
+    uint32) at `level` (wct_significance's quantile step, on the device): float64 [n_scales]."""
+    dev = _check_dev(hist)
+    hist = hist.contiguous()
+    if hist.dim() != 2 or hist.shape[0] < n_scales:
+        raise ValueError("hist must be [>= n_scales, nbins]")
+    out = torch.empty(max(n_scales, 1), dtype=torch.float64, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("wtmi_coherence_quantile", _ptr(hist), int(n_scales), int(hist.shape[1]), float(level),
+                  _ptr(out), _stream(dev))
+    return out[:n_scales]
 
 
 # -------------------------------------------------------------------------- MODWT

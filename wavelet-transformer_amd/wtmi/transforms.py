@@ -252,12 +252,13 @@ def wct_batch(y1: torch.Tensor, y2: torch.Tensor, dt, dj=1 / 12, s0=-1, J=-1, wa
     n0 = y1.shape[-1]
     sj, freqs = scales_for(n0, dt, dj, s0, J, wavelet)
     a1 = a2 = None
-    if normalize:
+    fused = normalize and 8 < n0 <= 16384  # normalised inside the transform's first kernel
+    if normalize and not fused:
         a1 = ops.series_affine(y1, ops.AFF_NORMALIZE)
         a2 = ops.series_affine(y2, ops.AFF_NORMALIZE)
     res = ops.wct_morlet(y1, y2, sj, dt, wavelet.f0, boxcar=boxcar_rows(wavelet, dj), affine1=a1,
                          affine2=a2, want_uv=want_uv, want_power=want_power,
-                         want_phase=want_phase, workspace=workspace)
+                         want_phase=want_phase, workspace=workspace, normalize=fused)
     return res, sj, freqs
 
 
@@ -475,10 +476,12 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
         coh = ops.wct_morlet(n1, n2, sj, dt, wavelet.f0, boxcar=K, want_uv=False, workspace=ws)["coh"]
         if maxscale > 0:
             ops.coherence_histogram(coh, lo, hi, maxscale, nbins, hist=hist)
-    wlc = _np(hist).view(np.uint32).astype(np.float64)
-    full = np.zeros((sj.size, nbins))
-    full[:wlc.shape[0]] = wlc[:maxscale] if maxscale > 0 else 0
-    sig95 = significance_from_histogram(full, anyout, maxscale, significance_level)
+    # the quantile step on the device (ops.coherence_quantile: the rule of
+    # significance_from_histogram); only maxscale levels come back
+    sig95 = np.zeros(sj.size)
+    sig95[anyout] = np.nan
+    if maxscale > 0:
+        sig95[:maxscale] = _np(ops.coherence_quantile(hist, maxscale, significance_level))
     if cache:
         sig_cache_store(key, sig95)
     return sig95
