@@ -4,9 +4,13 @@
 #      (copied into profiles/$ROUND/ on the box so the bench lines carry "traffic")
 #   2. rocprofv3 --kernel-trace --stats per config   -> gpurun_out/prof_<cfg>/
 #   3. bench.py per config (CPU baseline included)   -> gpurun_out/bench_<cfg>.json
+#   4. (r03) a VALU PMC pass per config + the traces -> gpurun_out/kernel_roofline.json
+#      (per-kernel binding resource; copied into profiles/$ROUND/ like pmc_traffic.json)
+#   PARTS selects the parts: "pmc prof roof bench" (default all).
 # Every GPU step has its own time limit; a crash / abort / timeout ends the session.
 set -u
-ROUND=${ROUND:-r02}
+ROUND=${ROUND:-r03}
+PARTS=${PARTS:-"pmc prof roof bench"}
 CFGS=${CFGS:-"c2 c3 c4 c5"}
 OUT=gpurun_out
 mkdir -p $OUT profiles/$ROUND
@@ -19,7 +23,8 @@ run() {  # name timeout cmd...
   echo "   rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; echo "FATAL in $name"; exit $rc; fi
 }
-if [ "${SKIP_PMC:-0}" != 1 ]; then
+has() { case " $PARTS " in *" $1 "*) return 0;; esac; return 1; }
+if has pmc; then
   for c in $CFGS; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
       run pmc_${c}_$ctr 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/pmc_${c}_$ctr -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
@@ -28,7 +33,7 @@ if [ "${SKIP_PMC:-0}" != 1 ]; then
   done
   cp $OUT/pmc_traffic.json profiles/$ROUND/pmc_traffic.json
 fi
-if [ "${SKIP_PROF:-0}" != 1 ]; then
+if has prof; then
   for c in $CFGS; do
     STEPS_K=10
     [ $c = c2 ] && STEPS_K=50
@@ -36,12 +41,24 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
     python scripts/trace_mean.py $OUT/prof_$c $STEPS_K > $OUT/prof_$c/timed_mean.txt
   done
 fi
-for c in $CFGS; do
-  ARGS=""
-  [ $c = c2 ] && ARGS="--steps 20 --warmup 5"
-  [ $c = c2 ] || ARGS="--steps 10 --warmup 3"
-  run bench_$c 600 python bench.py --config $c $ARGS
-  grep '^{' $OUT/bench_$c.log | tail -1 > $OUT/bench_$c.json
-  cut -c1-200 $OUT/bench_$c.json
-done
+if has roof; then
+  for c in $CFGS; do
+    run valu_$c 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/valu_$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
+    STEPS_K=10
+    [ $c = c2 ] && STEPS_K=50
+    python scripts/kernel_roofline.py $c $OUT/prof_$c $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/valu_$c $OUT/kernel_roofline.json $STEPS_K > $OUT/roof_$c.txt || exit 1
+    head -4 $OUT/roof_$c.txt
+  done
+  cp $OUT/kernel_roofline.json profiles/$ROUND/kernel_roofline.json
+fi
+if has bench; then
+  for c in $CFGS; do
+    ARGS=""
+    [ $c = c2 ] && ARGS="--steps 20 --warmup 5"
+    [ $c = c2 ] || ARGS="--steps 10 --warmup 3"
+    run bench_$c 600 python bench.py --config $c $ARGS
+    grep '^{' $OUT/bench_$c.log | tail -1 > $OUT/bench_$c.json
+    cut -c1-200 $OUT/bench_$c.json
+  done
+fi
 echo ALLDONE
