@@ -349,7 +349,9 @@ class C4(Workload):
         self.bytes = self.units * 12 + self.local * self.n * 8
         self.ws = torch.empty(self.ops.wct_workspace_bytes(max(self.local, 1), self.n, S),
                               dtype=torch.uint8, device=dev)
-        self.per_step = {"wtmi::wct_": 1, "wtmi::moments_kernel<": 2}
+        # every wtmi::wct_* kernel of the step once (r03: the normalisation runs inside
+        # wct_spectra_plan; no separate moments launches)
+        self.per_step = {"wtmi::wct_": 1}
         self.bytes_note = "12 B/coeff (|W12|^2 + WCT + phase, f32) + 8 B/pair-sample inputs"
 
     def step(self):

@@ -121,13 +121,15 @@ def gpu_side(args, y, t, y1, y2):
             geo = st("host geometry (noise length, COI intervals)",
                      lambda: transforms.wct_sig_geometry(wct.DT, wct.DJ, wct.S0, J))
             wlc = np.random.default_rng(0).integers(0, 50, (geo[1].size, 1000)).astype(float)
-            st("host quantile over the counter",
+            st("host quantile rule (restatement; the call itself runs it on the device)",
                lambda: transforms.significance_from_histogram(wlc, geo[4], geo[5]))
         out["run_wct_sig_steps_median_ms"] = {k: float(np.median(v)) for k, v in steps.items()}
         N = geo[0]
+        from wtmi import ops
+        per_pair = max(1, ops.wct_workspace_bytes(1, N, geo[1].size))
         out["sig_geometry"] = {"noise_samples": int(N), "scales": int(geo[1].size),
                                "maxscale": int(geo[5]), "passes": 300,
-                               "pairs_per_launch": 128}
+                               "pairs_per_launch": int(min(300, 512, (8 << 30) // per_pair))}
     return out
 
 
