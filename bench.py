@@ -332,9 +332,11 @@ class C4(Workload):
     """XWT + WCT: 512 pairs x 8192, dj = 1/8 -> 97 scales."""
     name, axis, seed = "c4", "pair", 1004
     B, n, dj = 512, 8192, 1 / 8
-    kernel = ("moments<float> x2 + wct_spectra<13> + wct_plan<13> + wct_phase_a<13,full-band rows> + "
-              "wct_dec_kernel<13,8..12> + wct_phase_a<13,decimated rows> + wct_wide_boxcar<10> + "
-              "wct_phase_c<13,q windows> + wct_phase_c<13,wide windows> + wct_phase_b<10>, one stream")
+    kernel = ("wct_spectra_plan<13> (normalisation in the load, plan in the last workgroup) + "
+              "wct_phase_a<13,full-band rows> [side stream] || wct_dec_kernel<13,8..12> + "
+              "wct_phase_a<13,decimated rows> + wct_phase_b<10> [caller's stream], "
+              "wct_wide_boxcar<10> + wct_phase_c<13,q windows> + wct_phase_c<13,wide windows> "
+              "[side stream]; joined on the caller's stream")
 
     def setup(self):
         from wtmi import transforms

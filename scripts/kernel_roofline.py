@@ -91,7 +91,7 @@ def main():
     if os.path.exists(out):
         with open(out) as fh:
             data = json.load(fh)
-    data[cfg] = {"kernels": rows, "method": __doc__.split("\n\n")[1].strip()}
+    data[cfg] = {"kernels": rows, "method": __doc__.split("\n\n")[2].strip()}
     with open(out, "w") as fh:
         json.dump(data, fh, indent=1)
     for r in rows:
