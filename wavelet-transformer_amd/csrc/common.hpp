@@ -52,6 +52,38 @@ __device__ __forceinline__ float fast_atan2f(float y, float x) {
   return copysignf(r, y);
 }
 
+// Two fast_atan2f at once (lane i of the vectors is atan2(y[i], x[i]), bitwise the scalar
+// function's result): the octant reduction stays scalar (no packed min/max/rcp on gfx950),
+// the polynomial runs on v_pk_fma_f32 -- 11 packed instructions for both values instead of
+// 22 scalar ones.
+__device__ __forceinline__ cpx fast_atan2f_x2(cpx y, cpx x) {
+  cpx a;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float ax = fabsf(x[i]), ay = fabsf(y[i]);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    a[i] = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+  }
+  const cpx s = a * a;
+  cpx p = cpx{-0.004781003575772047f, -0.004781003575772047f};
+  p = cfma(p, s, cpx{0.02455916814506054f, 0.02455916814506054f});
+  p = cfma(p, s, cpx{-0.059907760471105576f, -0.059907760471105576f});
+  p = cfma(p, s, cpx{0.0994298979640007f, 0.0994298979640007f});
+  p = cfma(p, s, cpx{-0.1402951329946518f, -0.1402951329946518f});
+  p = cfma(p, s, cpx{0.19971394538879395f, 0.19971394538879395f});
+  p = cfma(p, s, cpx{-0.3333209455013275f, -0.3333209455013275f});
+  p = cfma(p, s, cpx{0.9999999403953552f, 0.9999999403953552f});
+  cpx r = a * p;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float ri = r[i];
+    if (fabsf(y[i]) > fabsf(x[i])) ri = 1.57079632679489662f - ri;
+    if (x[i] < 0.f) ri = 3.14159265358979324f - ri;
+    r[i] = copysignf(ri, y[i]);
+  }
+  return r;
+}
+
 // Wave-uniform buffer resource for one output/input row (T8/T20 of the CDNA guide):
 // rows are addressed as SGPR descriptor + 32-bit per-lane voffset + SGPR soffset, so a
 // 16-position-per-thread row store needs one offset VGPR instead of 16 64-bit address

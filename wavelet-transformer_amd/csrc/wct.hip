@@ -236,8 +236,13 @@ template <int LOGN, bool BUF>
 __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16], long long rowbase, int t) {
   const int n0 = a.n0;
   if (a.out_pow) put_row<LOGN, BUF>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w[m]); });
-  if (a.out_sig)  // phase angle
-    put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return fast_atan2f(w[m].y, w[m].x); });
+  if (a.out_sig) {  // phase angle, two positions per packed polynomial
+    cpx ang[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      ang[m] = fast_atan2f_x2(cpx{w[2 * m].y, w[2 * m + 1].y}, cpx{w[2 * m].x, w[2 * m + 1].x});
+    put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return ang[m >> 1][m & 1]; });
+  }
   if (a.out_u) {
     put_row<LOGN, BUF>(a.out_u + rowbase, t, n0, [&](int m) {
       const float r = sqrtf(cabs2(w[m]));
