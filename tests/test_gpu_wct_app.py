@@ -295,6 +295,15 @@ def test_src_dwt_and_modwt(dwt_golden, modwt_golden):
         comp = dwt.reconstruct_signal_component(res.coeffs, dwt.MOTHER, 1)
         ref = g[f"c{i}_comp1"]
         assert np.abs(comp - ref).max() <= 1e-5 * max(np.abs(ref).max(), 1e-12)
+        # every component (served by the batched cache) bitwise equal to its own launch
+        from wtmi import transforms
+        for lvl in range(len(res.coeffs)):
+            got = dwt.reconstruct_signal_component(res.coeffs, dwt.MOTHER, lvl)
+            one = transforms.waverec_variants(res.coeffs, dwt.MOTHER, [1 << lvl])[0]
+            assert np.array_equal(got, one)
+            if f"c{i}_comp{lvl}" in g:
+                ref = g[f"c{i}_comp{lvl}"]
+                assert np.abs(got - ref).max() <= 1e-5 * max(np.abs(ref).max(), 1e-12)
     m = modwt_golden
     for i in range(int(m["ncases"])):
         x, w, J = m[f"c{i}_x"], m[f"c{i}_w"], int(m[f"c{i}_J"])

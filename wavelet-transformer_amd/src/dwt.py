@@ -9,7 +9,10 @@ keep pywt order ``[cA_J, cD_J, ..., cD_1]`` (quirk B.10).
 
 from __future__ import annotations
 
+import hashlib
 import logging
+import threading
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Type
 
@@ -112,9 +115,57 @@ def wavedec_batch(dwt_data_list: List[DataForDWT]) -> list:
     return out
 
 
+class _ComponentCache:
+    """All single-entry reconstructions of one coefficient list, from ONE batched launch.
+
+    The reference's callers reconstruct the components of a list one level at a time
+    (src/regression.py:113-114 alternates two lists over levels + 1 calls; src/dwt.py:123-156
+    loops too): the first call for a list computes every component in one ``waverec`` launch
+    (``n_variants`` = the list's length) and the others are served from here.  Keyed by the
+    coefficients' content (and the wavelet), so a list mutated in place is a new key; a few
+    lists are kept (least recently used dropped); thread-safe (Streamlit sessions share the
+    module)."""
+
+    def __init__(self, size: int = 8):
+        self.size = size
+        self._d: "OrderedDict[tuple, list]" = OrderedDict()
+        self._lock = threading.Lock()
+
+    @staticmethod
+    def key(coeffs: list, wavelet) -> tuple:
+        h = hashlib.blake2b(digest_size=16)
+        for c in coeffs:
+            a = np.ascontiguousarray(c)
+            h.update(str((a.dtype.str, a.shape)).encode())
+            h.update(a.tobytes())
+        w = as_filter_bank(wavelet)
+        return (h.hexdigest(), w.name, tuple(w.dec_lo))
+
+    def get(self, coeffs: list, wavelet, level: int):
+        k = self.key(coeffs, wavelet)
+        with self._lock:
+            parts = self._d.get(k)
+            if parts is not None:
+                self._d.move_to_end(k)
+        if parts is None:
+            parts = transforms.waverec_variants(coeffs, wavelet, [1 << j for j in range(len(coeffs))])
+            with self._lock:
+                self._d[k] = parts
+                self._d.move_to_end(k)
+                while len(self._d) > self.size:
+                    self._d.popitem(last=False)
+        return np.array(parts[level], copy=True)
+
+
+_COMPONENTS = _ComponentCache()
+
+
 def reconstruct_signal_component(signal_coeffs: list, wavelet: str, level: int):
-    """Inverse DWT keeping only list entry ``level`` (src/dwt.py:110-120)."""
-    return transforms.waverec_variants(signal_coeffs, wavelet, [1 << level])[0]
+    """Inverse DWT keeping only list entry ``level`` (src/dwt.py:110-120); every component
+    of the list comes from one batched launch on the first call (``_ComponentCache``)."""
+    if not 0 <= level < len(signal_coeffs):  # the reference zeroes every entry then
+        return transforms.waverec_variants(signal_coeffs, wavelet, [0])[0]
+    return _COMPONENTS.get(signal_coeffs, wavelet, level)
 
 
 def _subplots(nrows, **kwargs):
