@@ -1382,14 +1382,17 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
 // Rows per workgroup when the options leave them at 0 (auto): shorter workgroups for small
 // batches (one GPU's share of a strong-scaling run), so the grids still fill the CUs.  C4 rows
 // at 64 / 128 / 256 / 512 pairs, one box (ms, 4+4 rows -> this rule): 0.675 -> 0.600,
-// 1.075 -> 1.023, 1.914 -> 1.894, 3.54 unchanged.
+// 1.075 -> 1.023, 1.914 -> 1.894, 3.54 unchanged.  r03 sweep with the decimated rows' chunks
+// (wct_dec_rows; one box, two alternations, ms): 64 pairs (min 1, dec 2) 0.524-0.549 -> (1, 4)
+// 0.516-0.520 or (1, 8) 0.519-0.521; 128 (1, 2) 0.959-0.962 -> (2, 8) 0.924-0.927; 256 (2, 2)
+// 1.729-1.730 -> (2, 8) 1.694-1.697; 512 (4, 4) 3.227-3.236, (4, 8) 3.253-3.262, (2, 8) 3.34-3.38.
 static int wct_min_rows(long long batch) {
   const int o = options().wct_min_rows;
-  return o > 0 ? o : (batch <= 128 ? 1 : batch <= 256 ? 2 : 4);
+  return o > 0 ? o : (batch <= 64 ? 1 : batch <= 256 ? 2 : 4);
 }
 static int wct_dec_rows_per_wg(long long batch) {
   const int o = options().wct_dec_rows;
-  return o > 0 ? o : (batch <= 256 ? 2 : 4);
+  return o > 0 ? o : (batch <= 256 ? 8 : 4);
 }
 
 // Side stream of the calling thread on the current device (created once; thread_local, so
