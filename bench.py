@@ -7,15 +7,17 @@ Default workload = BASELINE config 2 (the metric's single-GPU config): batched M
 CWT, 1024 synthetic series x 4096 samples x 128 scales, fp32 in, complex64 W out,
 inputs resident in HBM, one step = one transform of the whole batch.
 
-Multi-GPU: the config's GLOBAL batch (C2 1024 series, C3 8192, C4 512
-pairs, C5 65536) is split into contiguous per-rank blocks (wtmi.sharding.shard_range),
-strong scaling, no collective on the data path; RCCL carries only the barrier and the
-max-over-ranks of the timed region.  ``--gpus N`` works two ways:
+Multi-GPU: series (pairs) are independent, so the units shard across ranks with
+no collective on the data path; RCCL carries only the barrier and the max-over-ranks of the
+timed region.  Default ``--scaling weak``: rank r transforms its own block [r B, (r + 1) B) of a
+global batch of N B series (B = the config's batch: C2 1024 series, C3 8192, C4 512 pairs, C5
+65536), distinct seeded data per rank, per-GPU work fixed as N grows.  ``--scaling strong``
+splits the config's batch B into contiguous per-rank blocks (wtmi.sharding.shard_range)
+instead (the shard-size measurements).  ``--gpus N`` works two ways:
   * under ``torch.distributed.run --nproc-per-node N`` (RANK/WORLD_SIZE in the env):
     this process is one rank; ``--gpus`` must equal WORLD_SIZE;
   * as a plain ``python bench.py --gpus N``: this process starts N fresh rank processes
     (before it, or they, touch the GPU), waits for them and exits with their status.
-``--scaling weak`` gives every rank the whole config batch instead.
 
 Clock ramp: the first few dozen launches after an idle period run ~10 % slower (C2:
 0.89 ms/step after 5 warm-up steps, 0.79 after 30 or 300, same box, same process
@@ -188,8 +190,8 @@ def synth_rows(seed, lo, hi, n, pairs=False):
 
 
 class Workload:
-    """One config's per-rank share: rows [lo, hi) of the global batch B (strong
-    scaling) or the whole batch on every rank (weak)."""
+    """One config's per-rank share: block [r B, (r + 1) B) of a global batch of N B rows
+    (weak scaling) or rows [lo, hi) of the batch B split over the ranks (strong)."""
     B = 0
     seed = 0
 
@@ -199,7 +201,7 @@ class Workload:
         self.ops, self.torch, self.dev = ops, torch, dev
         self.global_batch = self.B * (world if scaling == "weak" else 1)
         if scaling == "weak":
-            self.lo, self.hi = 0, self.B
+            self.lo, self.hi = rank * self.B, (rank + 1) * self.B
         else:
             self.lo, self.hi = sharding.shard_range(self.B, rank, world)
         self.local = self.hi - self.lo
@@ -521,7 +523,9 @@ def main():
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="keep warming up (untimed) until this many seconds have passed")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: every rank its own B-row block (per-GPU work fixed); strong: the "
+                         "config's B rows split over the ranks")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--cpu-per-worker", type=int, default=0, help="0 = per-config default")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1,8 +1,9 @@
-"""bench.py's multi-rank launcher and strong-scaling shards, on CPU (gloo, stub workload).
+"""bench.py's multi-rank launcher, weak (default) and strong scaling, on CPU (gloo, stub workload).
 
 `python bench.py --gpus N` must start N ranks itself when no torch.distributed.run
-environment is present, shard the config's GLOBAL batch contiguously, and report
-n_gpus = N with value = all ranks' units / max-over-ranks time.
+environment is present, give each rank its own block (weak: B rows per rank; strong: the
+config's B rows split contiguously), and report n_gpus = N with value = all ranks' units /
+max-over-ranks time.
 """
 
 import json
@@ -28,8 +29,8 @@ def _run(*args, env=None):
 
 
 @pytest.mark.parametrize("n,per_rank", [(1, 10), (2, 5), (3, 4)])
-def test_gpus_flag_launches_that_many_ranks(n, per_rank):
-    r, d = _run("--gpus", str(n))
+def test_gpus_flag_launches_that_many_ranks_strong(n, per_rank):
+    r, d = _run("--gpus", str(n), "--scaling", "strong")
     assert r.returncode == 0, r.stderr[-2000:]
     assert d["n_gpus"] == n and d["scaling"] == "strong"
     c = d["config"]
@@ -39,10 +40,14 @@ def test_gpus_flag_launches_that_many_ranks(n, per_rank):
     assert d["value"] == pytest.approx(10 * 256 * 3 / (d["ms_per_step"] * 3 / 1e3), rel=1e-6)
 
 
-def test_weak_scaling_gives_every_rank_the_whole_batch():
-    r, d = _run("--gpus", "2", "--scaling", "weak")
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_weak_scaling_is_the_default_one_block_per_rank(n):
+    r, d = _run("--gpus", str(n))
     assert r.returncode == 0, r.stderr[-2000:]
-    assert d["config"]["global_batch"] == 20 and d["config"]["per_rank_batch"] == 10
+    assert d["n_gpus"] == n and d["scaling"] == "weak"
+    c = d["config"]
+    assert c["global_batch"] == 10 * n and c["per_rank_batch"] == 10 and c["rank0_rows"] == [0, 10]
+    assert d["value"] == pytest.approx(10 * n * 256 * 3 / (d["ms_per_step"] * 3 / 1e3), rel=1e-6)
 
 
 def test_gpus_must_match_torchrun_world_size():

@@ -88,18 +88,20 @@ def test_two_ranks_on_one_gpu_gather_bitwise(tmp_path):
     torch.cuda.synchronize()
 
 
-def test_bench_two_ranks_gloo_smoke():
-    """bench.py --gpus 2 --dist-backend gloo: both ranks on the one GPU, the global C2
-    batch covered (512 series each), one JSON line with n_gpus 2."""
+@pytest.mark.parametrize("scaling,glob,per", [("strong", 1024, 512), ("weak", 2048, 1024)])
+def test_bench_two_ranks_gloo_smoke(scaling, glob, per):
+    """bench.py --gpus 2 --dist-backend gloo: both ranks on the one GPU; strong: the C2 batch
+    covered (512 series each); weak (the default): each rank its own 1024-series block; one
+    JSON line with n_gpus 2."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c2",
            "--dist-backend", "gloo", "--steps", "3", "--warmup", "1", "--prewarm-s", "0",
-           "--rank-timeout", "240"]
+           "--rank-timeout", "240", "--no-cpu-baseline", "--scaling", scaling]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
     cfg = line["config"]
-    assert cfg["global_batch"] == 1024 and cfg["per_rank_batch"] == 512
+    assert cfg["global_batch"] == glob and cfg["per_rank_batch"] == per
     assert cfg["dist_backend"] == "gloo"
     assert line["value"] > 0
     assert line["check"]["rank0_first_last_series_max_row_rel_err_vs_oracle"] < 1e-5
