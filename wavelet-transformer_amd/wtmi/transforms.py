@@ -331,6 +331,8 @@ def wct_sig_geometry(dt, dj, s0, J, wavelet="morlet"):
     if not anyout.any():
         raise ValueError("no scale has points outside the cone of influence")
     maxscale = int(np.nonzero(anyout)[0][-1])
+    if len(_GEOM_CACHE) >= 64:  # bounded: drop the oldest argument set (dicts keep order)
+        _GEOM_CACHE.pop(next(iter(_GEOM_CACHE)), None)
     _GEOM_CACHE[key] = (N, sj, t_lo, t_hi, anyout, maxscale)
     return N, sj.copy(), t_lo.copy(), t_hi.copy(), anyout.copy(), maxscale
 
