@@ -185,8 +185,12 @@ int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batc
  * rows, 0 full transforms), wct_target_wg, wct_min_rows and wct_dec_rows (scale rows per WCT
  * workgroup and decimated rows per phase-A workgroup; 0 = chosen by batch size), modwt_syn
  * (n = 8192 / 16384 synthesis: 1 hybrid kernel with the low levels staged through LDS, 0
- * dilation chains only).  The prune and kernel switches exist so that tests can compare the
- * paths; results agree to fp32 resolution either way.  The environment gives the process
+ * dilation chains only), wct_wide (0: windows touching a full-band row always take the
+ * time-domain path; 1..3: from which union-band exponent on they take the spectral route),
+ * wct_side_stream (1: the full-band rows' kernels on a per-thread side stream beside the
+ * decimated rows' chain), wct_direct (1: time-path rows with s/dt <= 4.15 smoothed by direct
+ * convolution instead of transforms; default 0, the transforms are faster).  The prune and kernel switches exist so that tests can
+ * compare the paths; results agree to fp32 resolution either way.  The environment gives the process
  * defaults; wtmi_set_option changes the CALLING thread's value only (thread-local), so it
  * never races a launch issued by another thread, and wtmi_get_option reads it back.
  * wtmi_set_option: 0, or -1 for an unknown name / out-of-range value;

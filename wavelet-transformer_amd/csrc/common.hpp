@@ -148,6 +148,10 @@ struct Options {
                             // from e >= wct_wide (1..3); 0 = never (time path)
   int wct_side_stream = 1;  // WTMI_WCT_SIDE_STREAM: full-band rows on a side stream beside the
                             // decimated rows' chain (1), or all on the caller's stream (0)
+  int wct_direct = 0;       // WTMI_WCT_DIRECT: time smoothing of the narrow-Gaussian time-path rows
+                            // (s/dt <= 4.15) by direct convolution in their own kernel (1), or by
+                            // transforms with the other full-band rows (0, default: faster on
+                            // MI355X at every measured size)
 };
 const Options& options();
 

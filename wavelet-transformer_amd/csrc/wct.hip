@@ -274,11 +274,25 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
 //                   (eu in 1..3: the window holds rows of regime q = 0 but none of band ew = 0),
 //                   its coherence comes from the WB spectra through one band inverse of Mu bins
 //                   per field instead of the time-domain workspace
+//   bit 18    direct time-path row (needT only, q = 0, not decimated) whose time Gaussian is narrow
+//                   (sigma = s/dt <= kDirectMaxSigma samples): smoothed by direct convolution with
+//                   the sampled Gaussian in phase A's kind-3 kernel instead of two transforms a field
 enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5,
-             kPlanNeedW = 128, kPlanDecShift = 8, kPlanEwShift = 12, kPlanEuShift = 16 };
+             kPlanNeedW = 128, kPlanDecShift = 8, kPlanEwShift = 12, kPlanEuShift = 16,
+             kPlanDirect = 1 << 18 };
 __device__ __forceinline__ int plan_dec(int pl) { return (pl >> kPlanDecShift) & 15; }
 __device__ __forceinline__ int plan_ew(int pl) { return (pl >> kPlanEwShift) & 15; }
 __device__ __forceinline__ int plan_eu(int pl) { return (pl >> kPlanEuShift) & 3; }
+// Direct smoothing (kPlanDirect): sigma <= 4.15 samples, taps |d| <= R with R + 1 >= kBandT sigma
+// (the dropped taps are below exp(-kBandT^2/2) = 6.8e-10 of the centre one, the criterion the
+// spectral routes use for the Gaussian's band); tap classes R = 18 (sigma <= 2.92) and R = 26;
+// rows of 1024 <= N <= 8192 (NT >= 64: a wave holds one row's taps, the halo fits the m = 0 / 15
+// slots)
+constexpr double kDirectMaxSigma = 4.15;
+constexpr int kDirectMinLogn = 10;
+constexpr int kDirectMaxLogn = 13;  // N = 16384: 1024-thread workgroups, 128 VGPRs, spills
+constexpr int kDirectR0 = 18, kDirectR1 = 26;
+constexpr int kDirectHalo = 32;
 // wide windows need M = N >> 3 >= 32 bins (one band phasor per thread): LOGN >= 8; the
 // spectral boxcar keeps K rows in registers: K <= 24
 constexpr int kWideMinLogn = 8;
@@ -337,8 +351,9 @@ __device__ __forceinline__ int plan_q(const double* scales, int r, double dt, do
 // decimated rows' list (S ints) and schedule (kDecSched ints), see wct_dec_kernel.
 template <int LOGN>
 __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales, int S, double dt, double f0,
-                                              int K, int prune, int dec, int wide, long long batch,
-                                              int* __restrict__ plan, int* __restrict__ scratch) {
+                                              int K, int prune, int dec, int wide, int direct,
+                                              long long batch, int* __restrict__ plan,
+                                              int* __restrict__ scratch) {
   __shared__ int last;
   if (threadIdx.x == 0) last = -1;
   const int LO = K / 2, HI = (K - 1) / 2;
@@ -376,7 +391,10 @@ __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales,
       else needT = true;
     }
     const int qw = qwin[r] & 15, eu = (qwin[r] >> 4) & 3;
+    const bool dir = direct && prune && LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn && q == 0 &&
+                     e == 0 && needT && !needS && !needW && scales[r] / dt <= kDirectMaxSigma;
     plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
+              (dir ? kPlanDirect : 0) |
               (needW ? kPlanNeedW : 0) |
               (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) |
               (eu >= 1 ? kPlanSpec | (eu << kPlanEuShift) : 0) |
@@ -432,9 +450,10 @@ __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales,
 template <int LOGN>
 __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra_plan(CwtArgs a, cpx* __restrict__ spec,
                                                                          int K, int dec, int wide,
-                                                                         int* __restrict__ plan) {
+                                                                         int direct, int* __restrict__ plan) {
   if (blockIdx.x + 1 == gridDim.x)
-    wct_plan_body<LOGN>(a.scales, a.S, a.dt, a.f0, K, a.prune, dec, wide, a.batch, plan, plan + a.S + 1);
+    wct_plan_body<LOGN>(a.scales, a.S, a.dt, a.f0, K, a.prune, dec, wide, direct, a.batch, plan,
+                        plan + a.S + 1);
   else
     spectra_body<LOGN>(a, spec, blockIdx.x);
 }
@@ -600,6 +619,131 @@ __device__ __forceinline__ void wct_dec_rows(const CwtArgs& a, const WctRowCtx& 
 //   Q = 0: W1, W2 -> z1 = |W1|^2 + i |W2|^2, W12 -> full smoothing transforms of both.
 //   Q >= 1: pruned inverse transforms, and once each forward transform is done only the one
 //   band bin per thread is kept (2 VGPRs), so W12's outputs and transforms run with z1 dead.
+// Time smoothing by direct convolution (plan bit kPlanDirect) of one field held in the FFT
+// layout (v[m] at position t + m NT): out[p] = sum_{|d| <= R} g[|d|] v[(p - d) mod N], g the
+// sampled Gaussian of the row times 1/s; lane d of the wave holds g[d] in gl, the taps are read
+// into SGPRs and broadcast by v_pk_fma_f32's op_sel.  The transforms' kernel ifft(F) / N is
+// that Gaussian periodised, up to the spectrum's cut at N/2 (below exp(-sigma^2 pi^2 / 2) = 3e-9
+// for sigma >= 2).  LDS copy of the row: position p at j = p + H (halos: positions [N - H, N) at
+// j < H, [0, H) at j >= N + H, so no window wraps), padded index j + j/32.  Thread u convolves
+// positions 16u .. 16u + 15 from the 16 + 2R positions around them: with u = 2u' + h the padded
+// index of 16u + q is A_h + (a compile-time offset of q), so every window read is one ds_read_b64
+// off one of two base registers, and for a fixed q the lanes' reads cover the 64 banks once per
+// half wave.  The result returns through LDS to the FFT layout, for put_row.
+template <int LOGN>
+struct DirectGeom {
+  static constexpr int EXTRA =
+      LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn ? 3 * kDirectHalo : 0;  // the halo copy's LDS
+};
+__host__ __device__ constexpr int floor32(int q) { return q >= 0 ? q / 32 : -((31 - q) / 32); }
+template <int LOGN, int R>
+__device__ __forceinline__ void direct_smooth(cpx (&v)[16], cpx* my, int t, int u, float gl) {
+  using P = FftPlan<LOGN>;
+  constexpr int H = kDirectHalo;
+  static_assert(R + 1 <= H && H <= P::NT && P::NT >= kWave, "halo covers the window, m = 0 / 15 slots");
+  __syncthreads();  // the row buffer's previous readers are done
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int j = t + m * P::NT + H;
+    my[j + (j >> 5)] = v[m];
+  }
+  if (t >= P::NT - H) {  // positions N - H .. N - 1 (m = 15) before the row
+    const int j = t + 15 * P::NT - P::N + H;
+    my[j + (j >> 5)] = v[15];
+  }
+  if (t < H) {  // positions 0 .. H - 1 (m = 0) after it
+    const int j = t + P::N + H;
+    my[j + (j >> 5)] = v[0];
+  }
+  __syncthreads();
+  float g[R + 1];
+#pragma unroll
+  for (int d = 0; d <= R; ++d)
+    g[d] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gl), d));
+  // padded index of position 16u + q: (q mod 32 < 16 ? A0 : A1) + q + R + 1 + floor(q / 32)
+  const int a0 = 16 * u + (u >> 1) + H + 1 - R - 1;
+  const cpx* b0 = my + a0;
+  const cpx* b1 = my + a0 + (u & 1);
+  cpx acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = mkc(0.f, 0.f);
+#pragma unroll
+  for (int q = -R; q < 16 + R; ++q) {
+    const cpx x = ((q - 32 * floor32(q)) < 16 ? b0 : b1)[q + R + 1 + floor32(q)];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int d = q < i ? i - q : q - i;
+      if (d <= R) acc[i] = cfma(x, mkc(g[d], g[d]), acc[i]);
+    }
+  }
+  __syncthreads();  // every window read is done before the row is overwritten
+  cpx* w0 = my + a0 + R + 1;  // position 16u + i at w0[i]
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w0[i] = acc[i];
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int j = t + m * P::NT + H;
+    v[m] = my[j + (j >> 5)];
+  }
+}
+
+template <int LOGN, bool BUF, int R>
+__device__ __forceinline__ void direct_fields(const CwtArgs& a, const WctRowCtx& c, cpx (&w1)[16], cpx (&v)[16],
+                                              cpx* my, int t, int u, float gl, bool valid, long long rowbase) {
+  direct_smooth<LOGN, R>(w1, my, t, u, gl);
+  if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, a.n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+  direct_smooth<LOGN, R>(v, my, t, u, gl);
+  if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, a.n0, [&](int m) { return v[m]; });
+}
+
+// Direct rows (plan bit kPlanDirect; phase A kind 3): W1, W2 by inverse transforms as the other
+// full-band rows, the XWT outputs, then both fields smoothed by direct convolution
+// (direct_smooth) into the time-domain workspace -- two transforms per row instead of six.
+template <int LOGN, bool FULL, bool TWL, int NZ>
+__device__ __forceinline__ void wct_rows_direct(const CwtArgs& a, const WctRowCtx& c, int r0, int r1, cpx* my,
+                                                const cpx* tw, int g, int t, int& par, const float4* twl) {
+  using P = FftPlan<LOGN>;
+  using G = WctGeom<LOGN>;
+  constexpr bool BUF = P::NT >= kWave;
+  const float f0 = static_cast<float>(a.f0);
+  const int n0 = a.n0;
+  const int u = static_cast<int>(threadIdx.x) - g * P::NT;
+  const float ln = static_cast<float>(__lane_id());
+  for (int r = r0; r < r1; r += G::ROWS) {
+    const int jl = r + g;
+    const bool valid = jl < r1;
+    const cpx prm = c.prm_tab[valid ? jl : r0];
+    const long long rowbase = (c.b * a.S + c.j0 + (valid ? jl : r0)) * static_cast<long long>(n0);
+    cpx w1[16], v[16];
+    wct_inverse_row<LOGN, 0, TWL, NZ>(v, c.spec1, prm, f0, my, tw, t, par, twl);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) w1[m] = v[m];
+    wct_inverse_row<LOGN, 0, TWL, NZ>(v, c.spec2, prm, f0, my, tw, t, par, twl);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {  // W12, z1 = |W1|^2 + i |W2|^2, zero past n0
+      const int pos = t + m * P::NT;
+      const cpx w12 = cmul(w1[m], cconj(v[m]));
+      const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
+      const bool in = FULL || pos < n0;
+      w1[m] = in ? w12 : mkc(0.f, 0.f);
+      v[m] = in ? z1 : mkc(0.f, 0.f);
+    }
+    if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
+    const double s = a.scales[c.j0 + (valid ? jl : r0)];
+    const double sg = s / a.dt;  // the Gaussian's sigma in samples
+    const float ce = static_cast<float>(-0.5 * 1.44269504088896340736 / (sg * sg));
+    const float amp = static_cast<float>(1.0 / (2.50662827463100050242 * sg * s));
+    const float gl = amp * __builtin_amdgcn_exp2f(ce * ln * ln);
+    // tap class of the iteration's widest row (rows ascend in scale; workgroup-uniform)
+    const double sg_max = a.scales[c.j0 + min(r + G::ROWS, r1) - 1] / a.dt;
+    if (sg_max * kBandT <= kDirectR0 + 1)
+      direct_fields<LOGN, BUF, kDirectR0>(a, c, w1, v, my, t, u, gl, valid, rowbase);
+    else
+      direct_fields<LOGN, BUF, kDirectR1>(a, c, w1, v, my, t, u, gl, valid, rowbase);
+  }
+}
+
 template <int LOGN, bool FULL, int Q, bool TWL, int NZ = 16>
 __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, int r0, int r1, cpx* my,
                                          const cpx* tw, int g, int t, int& par, const float4* twl) {
@@ -757,22 +901,28 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
 // other non-decimated rows (regimes 1, 2), 2 the decimated rows (plan e > 0).  Separate
 // launches over the same chunk grid, so that each row kind gets its own kernel's register
 // budget (one kernel for kinds 0 and 1 spilled 128 bytes per lane on LOGN 13, kind 0 alone 48).
+// 3 the direct rows (plan bit kPlanDirect, option wct_direct, off by default: full-band time-path
+// rows smoothed by direct convolution; their kernel takes the 256-VGPR budget of one 512-thread
+// workgroup per CU -- in the 128-VGPR kind-0 kernel the unrolled convolution spilled -- and is
+// slower than the transforms it replaces at every measured size).
 template <int LOGN> __device__ __forceinline__ int phase_a_kind(int pl) {
-  return plan_dec(pl) > 0 ? 2 : ((pl & kPlanQ) == 0 ? 0 : 1);
+  return plan_dec(pl) > 0 ? 2 : (pl & kPlanDirect) ? 3 : ((pl & kPlanQ) == 0 ? 0 : 1);
 }
 template <int LOGN, bool FULL, int KIND>
-__global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
+__global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (KIND == 3 ? 2 : WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB,
                 cpx* __restrict__ SB, const cpx* __restrict__ DY, cpx* __restrict__ WB,
                 const int* __restrict__ plan) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
   constexpr int BAND_F4 = LOGN >= 12 ? (P::N >> 8) : 1;  // 2 * (N >> 8) complex
-  __shared__ float4 lds4[(G::ROWS * P::PADN) / 2 + G::MAXCHUNK + G::TWL_F4 + G::MAXCHUNK / 4 + BAND_F4];
+  // row buffers: the FFT exchange (PADN), or for direct rows also the halo copy (direct_smooth)
+  constexpr int CSTR = P::PADN + (KIND == 3 ? DirectGeom<LOGN>::EXTRA : 0);
+  __shared__ float4 lds4[(G::ROWS * CSTR) / 2 + G::MAXCHUNK + G::TWL_F4 + G::MAXCHUNK / 4 + BAND_F4];
   cpx* lds = reinterpret_cast<cpx*>(lds4);
-  cpx* prm_tab = lds + G::ROWS * P::PADN;      // (alpha, log2 c) of the Morlet filter
+  cpx* prm_tab = lds + G::ROWS * CSTR;         // (alpha, log2 c) of the Morlet filter
   cpx* smt_tab = prm_tab + G::MAXCHUNK;        // (beta, 1/(N s)) of the time smoother
-  float4* twl = lds4 + (G::ROWS * P::PADN) / 2 + G::MAXCHUNK;
+  float4* twl = lds4 + (G::ROWS * CSTR) / 2 + G::MAXCHUNK;
   int* q_tab = reinterpret_cast<int*>(twl + G::TWL_F4);  // row regimes (wct_regime)
   const int tid = threadIdx.x;
   const int g = tid / P::NT;
@@ -783,7 +933,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   const int ch = static_cast<int>(blk - b * a.nchunks);
   const int j0 = ch * a.chunk;
   const int j1 = min(a.S, j0 + a.chunk);
-  cpx* my = lds + g * P::PADN;
+  cpx* my = lds + g * CSTR;
   {  // any rows of this launch's kind in the chunk?  (uniform: every thread reads the same plan)
     bool any = false;
     for (int r = j0; r < j1; ++r) any |= phase_a_kind<LOGN>(plan[r]) == KIND;
@@ -792,8 +942,8 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const int pl = plan[j0 + i];
-    // run key: the regime, or 4 + e for decimated rows
-    q_tab[i] = plan_dec(pl) > 0 ? 4 + plan_dec(pl) : (pl & kPlanQ);
+    // run key: the regime, 4 + e for decimated rows, 16 for direct rows
+    q_tab[i] = plan_dec(pl) > 0 ? 4 + plan_dec(pl) : (pl & kPlanDirect) ? 16 : (pl & kPlanQ);
     if (KIND == 2) continue;  // decimated rows need no filter tables
     const double s = a.scales[j0 + i];
     prm_tab[i] = morlet_params(s, a.dt, P::N);
@@ -833,7 +983,14 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     const int q = q_tab[r0];
     int r1 = r0 + 1;
     while (r1 < nrow && q_tab[r1] == q) ++r1;
-    if (q >= 4) {  // decimated rows (full rows only)
+    if (q == 16) {  // direct rows
+      if constexpr (KIND == 3 && LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) {
+        if (a.prune && a.f0 >= kBandF0 && P::NT >= 16)  // negative frequencies dropped: half the bins
+          wct_rows_direct<LOGN, FULL, TWL, 8>(a, c, r0, r1, my, tw, g, t, par, twl);
+        else
+          wct_rows_direct<LOGN, FULL, TWL, 16>(a, c, r0, r1, my, tw, g, t, par, twl);
+      }
+    } else if (q >= 4) {  // decimated rows (full rows only)
       if constexpr (KIND == 2 && FULL && LOGN >= kDecMinLogn) {
         switch (q - 4) {
 #define WTMI_DR(EE)                                                                     \
@@ -1448,8 +1605,11 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   if (grid > 0x7fffffffll || a.batch * a.S > 0x7fffffffll - 64) return kErrUnsupported;
   // decimated rows: full rows, pruning level 2, Morlet negative frequencies negligible
   const int dec = (a.prune >= 2 && a.n0 == (1 << LOGN) && LOGN >= kDecMinLogn && a.f0 >= kBandF0) ? 1 : 0;
+  // direct rows (kPlanDirect) and their kernel (phase A kind 3)
+  const int direct =
+      (options().wct_direct && a.prune && LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) ? 1 : 0;
   hipLaunchKernelGGL(wct_spectra_plan<LOGN>, dim3(static_cast<unsigned>(sgrid + 1)), dim3(G::BLOCK), 0, st, a,
-                     spec, K, dec, options().wct_wide, plan);
+                     spec, K, dec, options().wct_wide, direct, plan);
   int rc = launch_status();
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
@@ -1457,6 +1617,13 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
     hipLaunchKernelGGL((wct_phase_a<LOGN, false, 0>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
                        plan);
     if ((rc = launch_status()) != kOk) return rc;
+    if constexpr (LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) {
+      if (direct) {
+        hipLaunchKernelGGL((wct_phase_a<LOGN, false, 3>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY,
+                           WB, plan);
+        if ((rc = launch_status()) != kOk) return rc;
+      }
+    }
     if (a.prune) {  // band rows exist only with pruning
       hipLaunchKernelGGL((wct_phase_a<LOGN, false, 1>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
                          plan);
@@ -1475,6 +1642,13 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   hipLaunchKernelGGL((wct_phase_a<LOGN, true, 0>), gd, dim3(G::BLOCK), 0, sa, a, spec, TA, TB, SB, DY, WB,
                      plan);
   if ((rc = launch_status()) != kOk) return rc;
+  if constexpr (LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) {
+    if (direct) {
+      hipLaunchKernelGGL((wct_phase_a<LOGN, true, 3>), gd, dim3(G::BLOCK), 0, sa, a, spec, TA, TB, SB, DY, WB,
+                         plan);
+      if ((rc = launch_status()) != kOk) return rc;
+    }
+  }
   if (side && hipEventRecord(side->k0, side->s) != hipSuccess) return launch_status();
   // band rows that are not decimated: none when the decimation is on (a row of regime >= 1 has
   // its CWT band within N/16, hence a decimation M <= N/8), so that launch is skipped then
