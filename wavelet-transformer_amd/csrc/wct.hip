@@ -544,7 +544,17 @@ __device__ __forceinline__ void band_load(cpx (&pre)[8], const cpx* __restrict__
       for (int r = 0; r < B::NZ; ++r) pre[r] = g[t + r * P::NT + (r < B::NZ / 2 ? B::H : -B::H)];
     }
   } else {
-    pre[0] = t < B::M ? g[(t + B::H) & (B::M - 1)] : mkc(0.f, 0.f);
+    // per-row offsets, not hoisted: hoisted, one 64-bit address per band width and buffer
+    // (DY / TA / TB) stayed live across the row loop and spilled -- 9 x 8 bytes per lane
+    // written to scratch by every workgroup's prologue, 0.4 GB of C4's HBM writes
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+    if constexpr (P::NT >= kWave) {  // wave-uniform row: buffer load, lanes t >= M read 0
+      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(g, B::M * static_cast<int>(sizeof(cpx)));
+      pre[0] = buf_ld_c64(rs, tt < B::M ? 8 * ((tt + B::H) & (B::M - 1)) : 8 * B::M, 0);
+    } else {
+      pre[0] = tt < B::M ? g[(tt + B::H) & (B::M - 1)] : mkc(0.f, 0.f);
+    }
   }
 }
 
