@@ -1334,7 +1334,8 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
     asm volatile("" : "+v"(tt));  // per-row index math, not hoisted (register budget)
     const int k = tt - P::NT / 2;  // band-workspace index t <-> bin k
     const bool holder = k >= -K0 && k < K0;
-    const float wn = K > 1 ? 1.f / (K - 1) : 1.f;
+    float wn = K > 1 ? 1.f / (K - 1) : 1.f;
+    asm volatile("" : "+v"(wn));  // the window weights per row: hoisted, they spilled (prologue scratch)
     cpx yz = mkc(0.f, 0.f), yw = mkc(0.f, 0.f);
     if (holder) {
       // window rows in groups of U with every load of a group issued before its first
