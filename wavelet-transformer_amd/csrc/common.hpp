@@ -19,6 +19,29 @@ __device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return __builtin_elem
 // a * b = a.x b + a.y (i b) = fma(a.yy, (-b.y, b.x), a.xx * b)
 __device__ __forceinline__ cpx cmul(cpx a, cpx b) { return cfma(a.yy, b.yx * cpx{-1.f, 1.f}, a.xx * b); }
 __device__ __forceinline__ cpx cconj(cpx a) { return a * cpx{1.f, -1.f}; }
+// The same products in two packed instructions.  The compiler builds (-b.y, b.x) with a
+// separate multiply (or xor + mov): it does not fold a one-lane sign into the VOP3P neg_lo /
+// neg_hi source modifiers, which v_pk_{mul,fma}_f32 take for free.  Same roundings as cmul:
+// the results are bit-identical.  Plain VALU arithmetic (no hazard-bearing instructions);
+// used for the FFT twiddle products, where a third of the multiplies were sign shuffles.
+//   a * b       = fma(a.yy, (-b.y, b.x), a.xx * b)
+//   a * conj(b) = fma(a.yy, b.yx, (a.x b.x, -a.x b.y))
+// One asm block each: with two, the hazard recognizer (blind to what an asm block holds)
+// put an s_nop between them on every product.
+__device__ __forceinline__ cpx cmul2(cpx a, cpx b) {
+  cpx t, r;
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=v"(r), "=&v"(t) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ cpx cmul2_conj(cpx a, cpx b) {
+  cpx t, r;
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1]"
+      : "=v"(r), "=&v"(t) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ cpx cscale(cpx a, float s) { return a * s; }
 __device__ __forceinline__ float cabs2(cpx a) { return fmaf(a.x, a.x, a.y * a.y); }
 

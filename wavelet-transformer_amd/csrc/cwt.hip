@@ -232,7 +232,7 @@ __global__ void __launch_bounds__((CwtGeom<LOGN, MODE, VAR>::BLOCK), (NBUF == 2 
       for (int m = 0; m < 16; ++m) w1[m] = v[m];
       inverse(X2);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = cmul(w1[m], cconj(v[m]));
+      for (int m = 0; m < 16; ++m) v[m] = cmul2_conj(w1[m], v[m]);
     }
     if (!valid) continue;
     const int j = j0 + jl;
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(256) cwt_direct_kernel(CwtArgs a, int N) {
   cpx v = mkc(static_cast<float>(w[0].x), static_cast<float>(w[0].y));
   if constexpr (MODE == 1) {
     const cpx w2 = mkc(static_cast<float>(w[1].x), static_cast<float>(w[1].y));
-    v = cmul(v, cconj(w2));
+    v = cmul2_conj(v, w2);
   }
   const long long o = idx;
   if (a.out_w) a.out_w[o] = v;

@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(256) long_col_kernel(LongArgs a) {
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const long long n = c + (static_cast<long long>(t + m * P::NT) << log2n2);
-      const cpx w12 = cmul(v[m], cconj(v2[m]));
+      const cpx w12 = cmul2_conj(v[m], v2[m]);
       if (n < a.n0) {
         const long long o = rowbase + n;
         const float pw = cabs2(w12);

@@ -184,7 +184,7 @@ __device__ __forceinline__ void band_phasor(cpx (&v)[16], int t) {
   asm volatile("" : "+v"(t));  // recompute per row: hoisted, the phasors spill (WCT VGPR budget 128)
   const cpx ph = expi_frac(-K0 * t, P::N);
 #pragma unroll
-  for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
+  for (int m = 0; m < 16; ++m) v[m] = cmul2(v[m], ph);
 }
 
 // Smoothed row from its band bin: band exchange, inverse FFT from pass Q, time phasor
@@ -575,7 +575,7 @@ __device__ __forceinline__ void band_ifft(cpx (&v)[16], const cpx (&pre)[8], cpx
   asm volatile("" : "+v"(tt));  // per row, not hoisted (register budget)
   const cpx ph = expi_frac(-B::H * tt, P::N);
 #pragma unroll
-  for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ph);
+  for (int m = 0; m < 16; ++m) v[m] = cmul2(v[m], ph);
 }
 
 // Phase A rows [r0, r1) of decimation e = E: the decimated spectra (wct_dec_kernel) hold W12's
@@ -733,7 +733,7 @@ __device__ __forceinline__ void wct_rows_direct(const CwtArgs& a, const WctRowCt
 #pragma unroll
     for (int m = 0; m < 16; ++m) {  // W12, z1 = |W1|^2 + i |W2|^2, zero past n0
       const int pos = t + m * P::NT;
-      const cpx w12 = cmul(w1[m], cconj(v[m]));
+      const cpx w12 = cmul2_conj(w1[m], v[m]);
       const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
       const bool in = FULL || pos < n0;
       w1[m] = in ? w12 : mkc(0.f, 0.f);
@@ -790,7 +790,7 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       band_entry<LOGN, 2>(v, y2, my, t);
       fft_row<LOGN, 1, 1, TWL, 2>(v, my, 0, tw, t, par, twl);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) w1[m] = cmul(w1[m], cconj(v[m]));
+      for (int m = 0; m < 16; ++m) w1[m] = cmul2_conj(w1[m], v[m]);
       if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
       cpx zy = mkc(0.f, 0.f), wy = mkc(0.f, 0.f);
       const int k = t - P::NT / 2;  // band-workspace index t <-> bin k
@@ -843,7 +843,7 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int pos = t + m * P::NT;
-      const cpx w12 = cmul(w1[m], cconj(v[m]));
+      const cpx w12 = cmul2_conj(w1[m], v[m]);
       const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
       const bool in = FULL || pos < n0;
       w1[m] = in ? w12 : mkc(0.f, 0.f);
