@@ -12,6 +12,8 @@
 // The Morlet filter is evaluated in-register: no filter bank is read from HBM.  The same
 // kernels instantiated with VAR = 1 serve pycwt's other mothers (Paul, DOG / Mexican hat:
 // mother_filter, full transforms -- the band pruning is Morlet's).
+// plain twiddle products in this file's FFTs (fft_lds.hpp, kPkTwiddles)
+#define WTMI_PK_TWIDDLES 0
 #include "cwt_common.hpp"
 #include "long_path.hpp"
 

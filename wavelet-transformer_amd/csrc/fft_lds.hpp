@@ -330,6 +330,76 @@ __device__ __forceinline__ cpx opaque(cpx w) {
   return w;
 }
 
+// Twiddle products: cmul2 / cmul2_conj (two packed instructions each, common.hpp) unless the
+// translation unit defines WTMI_PK_TWIDDLES 0 before including this header.  The asm
+// products cut the WCT kernels' VALU by 5-9 % (C4 3.27 -> 3.1 ms) but cost the store-bound
+// CWT kernel ~1 % (0.792 -> 0.804 ms per C2 launch, A/B on one box; the hazard recognizer
+// pads each asm result's first reader with an s_nop), so cwt.hip keeps the plain products.
+#ifndef WTMI_PK_TWIDDLES
+#define WTMI_PK_TWIDDLES 1
+#endif
+constexpr bool kPkTwiddles = WTMI_PK_TWIDDLES != 0;
+
+// (plain products) v[r] *= w^r for r = 1..NZ-1 from the bases w, w^2, w^4, w^8 (inputs r >= NZ are zero
+// and stay untouched; NZ = 16: all 15).
+template <int DIR, int NZ>
+__device__ __forceinline__ void apply_tw16_w_nz_plain(cpx* v, cpx w1, cpx w2, cpx w4, cpx w8) {
+  w1 = twd<DIR>(w1);
+  if constexpr (NZ > 2) {
+    w2 = twd<DIR>(w2);
+    const cpx w3 = cmul(w1, w2);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], w3);
+    if constexpr (NZ > 4) {
+      w4 = twd<DIR>(w4);
+      const cpx w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
+      v[4] = cmul(v[4], w4);
+      v[5] = cmul(v[5], w5);
+      v[6] = cmul(v[6], w6);
+      v[7] = cmul(v[7], w7);
+      if constexpr (NZ > 8) {
+        w8 = twd<DIR>(w8);
+        v[8] = cmul(v[8], w8);
+        v[9] = cmul(v[9], cmul(w8, w1));
+        v[10] = cmul(v[10], cmul(w8, w2));
+        v[11] = cmul(v[11], cmul(w8, w3));
+        v[12] = cmul(v[12], cmul(w8, w4));
+        v[13] = cmul(v[13], cmul(w8, w5));
+        v[14] = cmul(v[14], cmul(w8, w6));
+        v[15] = cmul(v[15], cmul(w8, w7));
+      }
+    }
+  }
+  v[1] = cmul(v[1], w1);
+}
+
+// (plain products) Trailing radix-R pass, butterfly Q: v[r] *= (w_t * exp(2 pi i Q/16))^r, r = 1..R-1, from
+// the bases b = (w_t, w_t^2, w_t^4) (inverse sign; DIR < 0 conjugates).
+template <int R, int DIR, int Q>
+__device__ __forceinline__ void apply_tw_tail_plain(cpx* v, const cpx* b) {
+  if constexpr (R == 2) {
+    v[1] = cmul(v[1], rot16<DIR, Q>(twd<DIR>(b[0])));
+  } else if constexpr (R == 4) {
+    const cpx w1 = rot16<DIR, Q>(twd<DIR>(b[0]));
+    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(b[1]));
+    v[1] = cmul(v[1], w1);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], cmul(w1, w2));
+  } else {
+    const cpx w1 = rot16<DIR, Q>(twd<DIR>(b[0]));
+    const cpx w2 = rot16<DIR, 2 * Q>(twd<DIR>(b[1]));
+    const cpx w4 = rot16<DIR, 4 * Q>(twd<DIR>(b[2]));
+    const cpx w3 = cmul(w1, w2);
+    v[1] = cmul(v[1], w1);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], w3);
+    v[4] = cmul(v[4], w4);
+    v[5] = cmul(v[5], cmul(w4, w1));
+    v[6] = cmul(v[6], cmul(w4, w2));
+    v[7] = cmul(v[7], cmul(w4, w3));
+  }
+}
+
 // v[r] *= w^r for r = 1..NZ-1 from the bases w, w^2, w^4, w^8 (inputs r >= NZ are zero
 // and stay untouched; NZ = 16: all 15).  The powers are derived in the inverse sign and the
 // forward transform multiplies by their conjugates (cmul2_conj): no conjugation of the bases.
@@ -338,6 +408,10 @@ __device__ __forceinline__ cpx twmul(cpx v, cpx w) { return DIR > 0 ? cmul2(v, w
 
 template <int DIR, int NZ>
 __device__ __forceinline__ void apply_tw16_w_nz(cpx* v, cpx w1, cpx w2, cpx w4, cpx w8) {
+  if constexpr (!kPkTwiddles) {
+    apply_tw16_w_nz_plain<DIR, NZ>(v, w1, w2, w4, w8);
+    return;
+  }
   if constexpr (NZ > 2) {
     const cpx w3 = cmul2(w1, w2);
     v[2] = twmul<DIR>(v[2], w2);
@@ -388,7 +462,9 @@ __device__ __forceinline__ void apply_tw16_lds(cpx* v, const float4* tab, int id
 // conj(w) exp(-2 pi i Q/16) = conj(w exp(2 pi i Q/16))).
 template <int R, int DIR, int Q>
 __device__ __forceinline__ void apply_tw_tail(cpx* v, const cpx* b) {
-  if constexpr (R == 2) {
+  if constexpr (!kPkTwiddles) {
+    apply_tw_tail_plain<R, DIR, Q>(v, b);
+  } else if constexpr (R == 2) {
     v[1] = twmul<DIR>(v[1], rot16<1, Q>(b[0]));
   } else if constexpr (R == 4) {
     const cpx w1 = rot16<1, Q>(b[0]);
