@@ -17,6 +17,9 @@
  *     calls can be captured into a hipGraph;
  *   - return value: 0 success, -1 invalid argument, -2 unsupported size,
  *     > 0 a hipError_t from the kernel launch;
+ *   - an empty batch (batch == 0, or no samples / scales where a size may be 0) is a
+ *     no-op returning 0 once the sizes are valid, and its array pointers may then be NULL
+ *     (an empty torch tensor has no storage; a rank's shard of a small batch can be empty);
  *   - calls are stateless and thread-safe.
  */
 #ifndef WTMI_H

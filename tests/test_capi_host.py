@@ -54,6 +54,41 @@ def test_invalid_arguments_rejected_without_gpu():
         _lib.call("wtmi_affine", None, 0, 1, 1, 1, None, None, 0, 1, None)
 
 
+def test_empty_batch_is_a_noop_without_gpu():
+    """include/wtmi.h: an empty batch returns 0 once the sizes are valid, with NULL arrays
+    (what an empty torch tensor hands over, e.g. a rank's empty shard of a small batch);
+    no launch happens, so this runs without a GPU.  Negative sizes still fail."""
+    import ctypes as C
+    from wtmi import _lib
+    lib = _lib.load()
+    lo = (C.c_double * 8)(*([0.125] * 8))
+    hi = (C.c_double * 8)(*([0.125, -0.125] * 4))
+    lo_p, hi_p = C.cast(lo, C.c_void_p), C.cast(hi, C.c_void_p)
+    masks = (C.c_ulonglong * 1)(1)
+    N = None
+    assert lib.wtmi_cwt_morlet(N, 16, 0, 16, N, N, 4, 1.0, 6.0, N, 0, N, N, N, N, N) == 0
+    assert lib.wtmi_cwt_mother(N, 16, 0, 16, N, N, 4, 1.0, 0, 6.0, N, 0, N, N, N, N, N) == 0
+    assert lib.wtmi_cwt_mother(N, 16, 3, 16, N, N, 0, 1.0, 0, 6.0, N, 0, N, N, N, N, N) == 0  # no scales
+    assert lib.wtmi_xwt_mother(N, N, 16, 0, 16, N, N, N, 4, 1.0, 0, 6.0, N, 0, N, N, N, N, N, N, N) == 0
+    assert lib.wtmi_wct_morlet(N, N, 16, 0, 16, N, N, N, 4, 1.0, 6.0, 3, N, N, N, N, N, N, N) == 0
+    assert lib.wtmi_wct_morlet_norm(N, N, 16, 0, 16, N, 4, 1.0, 6.0, 3, N, N, N, N, N, N, N) == 0
+    assert lib.wtmi_modwt(N, 16, 0, 16, lo_p, hi_p, 8, 2, N, N, N) == 0
+    assert lib.wtmi_imodwt(N, 0, 16, lo_p, hi_p, 8, 2, 3, N, 16, N, N) == 0
+    assert lib.wtmi_wavedec(N, 16, 0, 16, lo_p, hi_p, 8, 1, N, N, N) == 0
+    assert lib.wtmi_waverec(N, 0, 16, lo_p, hi_p, 8, 1, C.cast(masks, C.c_void_p), 1, N, 16, N, N) == 0
+    assert lib.wtmi_series_moments(N, 0, 16, 0, 16, N, N) == 0
+    assert lib.wtmi_series_affine(N, 0, 16, 0, 16, 1, N, N, N) == 0
+    assert lib.wtmi_affine(N, 0, 16, 0, 16, N, N, 0, 16, N) == 0
+    assert lib.wtmi_rednoise(N, 16, 0, 16, 0.5, 1, 0, N) == 0
+    assert lib.wtmi_coherence_histogram(N, 0, 16, 4, N, N, 4, 1000, N, N) == 0
+    assert lib.wtmi_coherence_quantile(N, 0, 1000, 0.95, N, N) == 0
+    # sizes are still validated first, and a non-empty batch still needs its arrays
+    assert lib.wtmi_cwt_morlet(N, 16, -1, 16, N, N, 4, 1.0, 6.0, N, 0, N, N, N, N, N) == -1
+    assert lib.wtmi_modwt(N, 16, 0, 16, N, N, 8, 2, N, N, N) == -1  # the filter bank is host data
+    assert lib.wtmi_wct_morlet(N, N, 16, 0, 16, N, N, N, 4, 1.0, 6.0, 0, N, N, N, N, N, N, N) == -1
+    assert lib.wtmi_modwt(N, 16, 1, 16, lo_p, hi_p, 8, 2, N, N, N) == -1
+
+
 def test_dwt_lengths_match_pywt_convention(dwt_golden):
     from wtmi import ops
     from oracle import dwt_spec as ds

@@ -380,8 +380,10 @@ extern "C" int wtmi_cwt_mother(const float* x, long long ld, long long batch, lo
                                double dt, int mother, double param, const double* sig_scale,
                                long long sig_ld, float* out_w, float* out_power, float* out_sig,
                                void* workspace, void* stream) {
-  if (!x || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
+  if (n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
   if (sig_ld != 0 && sig_ld < n_scales) return kErrArg;
+  if (batch == 0 || n0 == 0 || n_scales == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x || !scales) return kErrArg;
   if (!out_w && !out_power && !out_sig) return kErrArg;
   if (out_sig && !sig_scale) return kErrArg;
   if (n0 > (1ll << kLongMaxLog)) return kErrUnsupported;
@@ -421,8 +423,10 @@ extern "C" int wtmi_xwt_mother(const float* x1, const float* x2, long long ld, l
                                const double* sig_scale, long long sig_ld, float* out_w12,
                                float* out_power, float* out_sig, float* out_u, float* out_v,
                                void* workspace, void* stream) {
-  if (!x1 || !x2 || !scales || n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
+  if (n0 < 0 || batch < 0 || n_scales < 0 || ld < n0) return kErrArg;
   if (sig_ld != 0 && sig_ld < n_scales) return kErrArg;
+  if (batch == 0 || n0 == 0 || n_scales == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x1 || !x2 || !scales) return kErrArg;
   if (!out_w12 && !out_power && !out_sig && !out_u) return kErrArg;
   if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
   if (out_sig && !sig_scale) return kErrArg;

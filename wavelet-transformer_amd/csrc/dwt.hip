@@ -295,10 +295,11 @@ extern "C" int wtmi_wavedec(const float* x, long long ld, long long batch, long 
                             const double* dec_lo, const double* dec_hi, int n_taps, int level,
                             float* coeffs, void* workspace, void* stream) {
   DwtBank fb;
-  if (!x || !coeffs || batch < 0 || n < 1 || ld < n || level < 0 || level > 60) return kErrArg;
+  if (batch < 0 || n < 1 || ld < n || level < 0 || level > 60) return kErrArg;
   if (!make_dwt_bank(dec_lo, dec_hi, n_taps, fb)) return kErrArg;
   if (n > kDwtLongMaxN || batch > 0x7fffffffll) return kErrUnsupported;
-  if (batch == 0) return kOk;
+  if (batch == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x || !coeffs) return kErrArg;
   const long long total = dwt_lengths(n, n_taps, level, nullptr);
   if (n > kDwtMaxN) {
     if (!workspace) return kErrArg;
@@ -318,12 +319,11 @@ extern "C" int wtmi_waverec(const float* coeffs, long long batch, long long n, c
                             const unsigned long long* keep_masks, int n_variants, float* out,
                             long long out_len, void* workspace, void* stream) {
   DwtBank fb;
-  if (!coeffs || !out || !keep_masks || batch < 0 || n < 1 || level < 0 || level > 60 ||
-      n_variants < 1 || out_len < 1)
-    return kErrArg;
+  if (batch < 0 || n < 1 || level < 0 || level > 60 || n_variants < 1 || out_len < 1) return kErrArg;
   if (!make_dwt_bank(rec_lo, rec_hi, n_taps, fb)) return kErrArg;
   if (n > kDwtLongMaxN || batch * n_variants > 0x7fffffffll) return kErrUnsupported;
-  if (batch == 0) return kOk;
+  if (batch == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!coeffs || !out || !keep_masks) return kErrArg;
   const long long total = dwt_lengths(n, n_taps, level, nullptr);
   if (n > kDwtMaxN && level > 0) {
     if (!workspace) return kErrArg;

@@ -883,10 +883,11 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
                           const double* dec_lo, const double* dec_hi, int n_taps, int level,
                           float* w, void* workspace, void* stream) {
   FilterBank fb;
-  if (!x || !w || batch < 0 || n < 1 || ld < n || level < 1 || level > 62) return kErrArg;
+  if (batch < 0 || n < 1 || ld < n || level < 1 || level > 62) return kErrArg;
   if (!make_bank(dec_lo, dec_hi, n_taps, fb)) return kErrArg;
   if (n > kModwtLongMaxN || batch > 0x7fffffffll) return kErrUnsupported;
-  if (batch == 0) return kOk;
+  if (batch == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x || !w) return kErrArg;
   if (n > kModwtMaxN) {
     if (!workspace) return kErrArg;
     return modwt_long(x, ld, batch, static_cast<int>(n), fb, n_taps, level, w, static_cast<float*>(workspace),
@@ -928,10 +929,11 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
                            const double* dec_hi, int n_taps, int level, unsigned long long keep_mask,
                            float* x, long long ld_out, void* workspace, void* stream) {
   FilterBank fb;
-  if (!x || !w || batch < 0 || n < 1 || ld_out < n || level < 1 || level > 62) return kErrArg;
+  if (batch < 0 || n < 1 || ld_out < n || level < 1 || level > 62) return kErrArg;
   if (!make_bank(dec_lo, dec_hi, n_taps, fb)) return kErrArg;
   if (n > kModwtLongMaxN || batch > 0x7fffffffll) return kErrUnsupported;
-  if (batch == 0) return kOk;
+  if (batch == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x || !w) return kErrArg;
   if (n > kModwtMaxN) {
     if (!workspace) return kErrArg;
     return imodwt_long(w, batch, static_cast<int>(n), fb, n_taps, level, keep_mask, x, ld_out,

@@ -118,25 +118,29 @@ static int launch_moments(const void* x, int x_is_f64, long long ld, long long b
 
 extern "C" int wtmi_series_moments(const void* x, int x_is_f64, long long ld, long long batch,
                                    long long n, double* out, void* stream) {
-  if (!x || !out || batch < 0 || n < 1 || ld < n || n > 0x7fffffff) return kErrArg;
+  if (batch < 0 || n < 1 || ld < n || n > 0x7fffffff) return kErrArg;
+  if (batch == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x || !out) return kErrArg;
   return launch_moments(x, x_is_f64, ld, batch, n, out, 0, nullptr, stream);
 }
 
 extern "C" int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batch, long long n,
                                   int mode, double* moments, double* affine, void* stream) {
-  if (!x || !affine || batch < 0 || n < 1 || ld < n || n > 0x7fffffff || mode < 0 || mode > 7 ||
+  if (batch < 0 || n < 1 || ld < n || n > 0x7fffffff || mode < 0 || mode > 7 ||
       ((mode & kAffDetrend) && (mode & kAffRemoveMean)))
     return kErrArg;
+  if (batch == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x || !affine) return kErrArg;
   return launch_moments(x, x_is_f64, ld, batch, n, moments, mode, affine, stream);
 }
 
 extern "C" int wtmi_affine(const void* x, int x_is_f64, long long ld_in, long long batch, long long n,
                            const double* coef, void* y, int y_is_f64, long long ld_out,
                            void* stream) {
-  if (!x || !coef || !y || batch < 0 || n < 0 || ld_in < n || ld_out < n || n > 0x7fffffff)
-    return kErrArg;
+  if (batch < 0 || n < 0 || ld_in < n || ld_out < n || n > 0x7fffffff) return kErrArg;
   const long long total = batch * n;
-  if (total == 0) return kOk;
+  if (total == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x || !coef || !y) return kErrArg;
   const long long blocks = (total + 255) / 256;
   if (blocks > 0x7fffffffll) return kErrUnsupported;
   hipStream_t st = static_cast<hipStream_t>(stream);

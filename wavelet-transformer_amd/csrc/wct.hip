@@ -1943,12 +1943,11 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
                            const double* affine1, const double* affine2, int norm, const double* scales,
                            int n_scales, double dt, double f0, int boxcar, void* workspace, float* out_coh,
                            float* out_power, float* out_phase, float* out_u, float* out_v, void* stream) {
-  if (!x1 || !x2 || !scales || !workspace || !out_coh || n0 < 0 || batch < 0 || n_scales < 0 ||
-      ld < n0 || boxcar < 1)
-    return kErrArg;
-  if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
+  if (n0 < 0 || batch < 0 || n_scales < 0 || ld < n0 || boxcar < 1) return kErrArg;
   if (n0 > (1ll << kLongMaxLog)) return kErrUnsupported;
-  if (batch == 0 || n0 == 0 || n_scales == 0) return kOk;
+  if (batch == 0 || n0 == 0 || n_scales == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!x1 || !x2 || !scales || !workspace || !out_coh) return kErrArg;
+  if ((out_u == nullptr) != (out_v == nullptr)) return kErrArg;
   const int logn = log2_ceil_w(n0);
   CwtArgs a{};
   a.x = x1;

@@ -219,9 +219,10 @@ using namespace wtmi;
 
 extern "C" int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g,
                              unsigned long long seed, unsigned long long first_series, void* stream) {
-  if (!out || count < 0 || n < 0 || ld < n || !(g > -1.0 && g < 1.0)) return kErrArg;
+  if (count < 0 || n < 0 || ld < n || !(g > -1.0 && g < 1.0)) return kErrArg;
   if (n > (1ll << 30)) return kErrUnsupported;
-  if (count == 0 || n == 0) return kOk;
+  if (count == 0 || n == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
+  if (!out) return kErrArg;
   int tau = 0;
   if (g != 0.0) {
     const double tt = ceil(-2.0 / log(fabs(g)));
@@ -238,11 +239,11 @@ extern "C" int wtmi_rednoise(float* out, long long ld, long long count, long lon
 extern "C" int wtmi_coherence_histogram(const float* coh, long long batch, long long n0, int n_scales,
                                         const int* t_lo, const int* t_hi, int n_hist_scales, int nbins,
                                         unsigned* hist, void* stream) {
-  if (!coh || !t_lo || !t_hi || !hist || batch < 0 || n0 < 0 || n_scales < 0 || n_hist_scales < 0 ||
-      n_hist_scales > n_scales || nbins < 1)
+  if (batch < 0 || n0 < 0 || n_scales < 0 || n_hist_scales < 0 || n_hist_scales > n_scales || nbins < 1)
     return kErrArg;
   if (nbins > kMaxBins) return kErrUnsupported;
-  if (batch == 0 || n0 == 0 || n_hist_scales == 0) return kOk;
+  if (batch == 0 || n0 == 0 || n_hist_scales == 0) return kOk;  // empty: no-op (NULL arrays allowed)
+  if (!coh || !t_lo || !t_hi || !hist) return kErrArg;
   // enough blocks to fill the chip: split each scale's pairs into parts
   long long parts = (2048 + n_hist_scales - 1) / n_hist_scales;
   if (parts > batch) parts = batch;
@@ -257,8 +258,9 @@ extern "C" int wtmi_coherence_histogram(const float* coh, long long batch, long 
 
 extern "C" int wtmi_coherence_quantile(const unsigned int* hist, int n_scales, int nbins, double level,
                                        double* out, void* stream) {
-  if (!hist || !out || n_scales < 0 || nbins < 1 || !(level >= 0.0 && level <= 1.0)) return kErrArg;
-  if (n_scales == 0) return kOk;
+  if (n_scales < 0 || nbins < 1 || !(level >= 0.0 && level <= 1.0)) return kErrArg;
+  if (n_scales == 0) return kOk;  // empty: no-op (NULL arrays allowed)
+  if (!hist || !out) return kErrArg;
   hipLaunchKernelGGL(coherence_quantile_kernel, dim3(static_cast<unsigned>(n_scales)), dim3(kQThreads), 0,
                      static_cast<hipStream_t>(stream), hist, nbins, level, out);
   return launch_status();
