@@ -42,6 +42,31 @@ def test_c2_full_batch():
     torch.cuda.empty_cache()
 
 
+def test_c2_full_batch_linearity_every_series():
+    """C2 at full size through a size-independent property, on EVERY (series, scale) row:
+    the transform is linear, W(x + 2y) = W(x) + 2 W(y), to fp32 rounding (row-normwise
+    <= 1e-5 of ||W(x)|| + 2 ||W(y)||).  Catches a wrong row offset, a skipped chunk or a
+    grid-dependent path anywhere in the 4.3 GB output, which the sampled rows above cannot."""
+    from wtmi import ops
+    B, n, dj, J = 1024, 4096, 1 / 12, 127
+    x = torch.tensor(red_batch(1012, B, n), device="cuda")
+    y = torch.tensor(red_batch(2012, B, n), device="cuda")
+    sj = 2 * DT * 2 ** (np.arange(J + 1) * dj)
+    wx = ops.cwt_morlet(x, sj, DT)["w"]
+    wy = ops.cwt_morlet(y, sj, DT)["w"]
+    wz = ops.cwt_morlet(x + 2 * y, sj, DT)["w"]
+    worst = 0.0
+    for c in range(0, B, 128):
+        d = torch.linalg.vector_norm(wz[c:c + 128] - wx[c:c + 128] - 2 * wy[c:c + 128], dim=-1)
+        s = (torch.linalg.vector_norm(wx[c:c + 128], dim=-1)
+             + 2 * torch.linalg.vector_norm(wy[c:c + 128], dim=-1))
+        assert bool((s > 0).all())
+        worst = max(worst, (d / s).max().item())
+    assert worst <= 1e-5, worst
+    del wx, wy, wz
+    torch.cuda.empty_cache()
+
+
 def test_c5_full_chunk():
     """C5: one full 512-series streaming chunk, 8192 samples x 256 scales (dj = 1/24)."""
     from wtmi import ops
