@@ -130,3 +130,28 @@ def test_c4_full_batch():
         assert np.abs(dphi[mask]).max() <= 1e-4, p
     del res
     torch.cuda.empty_cache()
+
+
+def test_c4_full_batch_properties_every_pair():
+    """C4 at full size through size-independent properties, on EVERY pair, scale and sample:
+    a series is fully coherent with itself (WCT(x, x) = 1) and coherence is symmetric
+    (WCT(x, y) = WCT(y, x)), both to fp32 rounding (abs <= 1e-4, the coherence tolerance)."""
+    from wtmi import transforms
+    P, n, dj = 512, 8192, 1 / 8
+    y1 = torch.tensor(red_batch(1014, P, n), device="cuda")
+    y2 = torch.tensor((0.6 * np.roll(red_batch(1014, P, n), 3, axis=1)
+                       + 0.8 * red_batch(2014, P, n)).astype(np.float32), device="cuda")
+
+    def coh(a, b):
+        return transforms.wct_batch(a, b, DT, dj, 2 * DT, -1, want_uv=False)[0]["coh"]
+
+    c = coh(y1, y1)
+    assert c.shape == (P, 97, n)
+    assert (c - 1).abs().max().item() <= 1e-4
+    del c
+    cxy = coh(y1, y2)
+    cyx = coh(y2, y1)
+    assert bool(torch.isfinite(cxy).all())
+    assert (cxy - cyx).abs().max().item() <= 1e-4
+    del cxy, cyx
+    torch.cuda.empty_cache()
