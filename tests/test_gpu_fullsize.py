@@ -42,15 +42,17 @@ def test_c2_full_batch():
     torch.cuda.empty_cache()
 
 
-def test_c2_full_batch_linearity_every_series():
-    """C2 at full size through a size-independent property, on EVERY (series, scale) row:
-    the transform is linear, W(x + 2y) = W(x) + 2 W(y), to fp32 rounding (row-normwise
-    <= 1e-5 of ||W(x)|| + 2 ||W(y)||).  Catches a wrong row offset, a skipped chunk or a
-    grid-dependent path anywhere in the 4.3 GB output, which the sampled rows above cannot."""
+@pytest.mark.parametrize("B,n,dj,J", [(1024, 4096, 1 / 12, 127), (512, 8192, 1 / 24, 255)],
+                         ids=["c2_batch", "c5_chunk"])
+def test_cwt_full_size_linearity_every_series(B, n, dj, J):
+    """C2's batch and a C5 chunk at full size through a size-independent property, on EVERY
+    (series, scale) row: the transform is linear, W(x + 2y) = W(x) + 2 W(y), to fp32 rounding
+    (row-normwise <= 1e-5 of ||W(x)|| + 2 ||W(y)||).  Catches a wrong row offset, a skipped
+    chunk or a grid-dependent path anywhere in the 4.3 / 8.6 GB output, which the sampled rows
+    above cannot."""
     from wtmi import ops
-    B, n, dj, J = 1024, 4096, 1 / 12, 127
-    x = torch.tensor(red_batch(1012, B, n), device="cuda")
-    y = torch.tensor(red_batch(2012, B, n), device="cuda")
+    x = torch.tensor(red_batch(1012 + n, B, n), device="cuda")
+    y = torch.tensor(red_batch(2012 + n, B, n), device="cuda")
     sj = 2 * DT * 2 ** (np.arange(J + 1) * dj)
     wx = ops.cwt_morlet(x, sj, DT)["w"]
     wy = ops.cwt_morlet(y, sj, DT)["w"]
