@@ -105,6 +105,13 @@ def test_c3_full_batch():
         assert np.abs(back - x[r]).max() <= 1e-5 * np.abs(x[r]).max(), r
     err = ((xr - xd).abs().amax(dim=1) / xd.abs().amax(dim=1)).max().item()
     assert err <= 1e-5, err  # every series' round trip
+    # energy (MODWT with an orthonormal filter: sum_j ||W_j||^2 + ||V_J||^2 = ||x||^2), every series
+    worst = 0.0
+    for c in range(0, B, 512):
+        e_c = C[c:c + 512].double().square().sum(dim=(1, 2))
+        e_x = xd[c:c + 512].double().square().sum(dim=1)
+        worst = max(worst, ((e_c - e_x).abs() / e_x).max().item())
+    assert worst <= 1e-5, worst
     del C, xr
     torch.cuda.empty_cache()
 
