@@ -348,6 +348,8 @@ class C4(Workload):
         self.y1 = torch.tensor(y1, device=dev)
         self.y2 = torch.tensor(y2, device=dev)
         self.sj, _ = transforms.scales_for(self.n, DT, self.dj, 2 * DT, -1, transforms.as_morlet(None))
+        self.sjd = torch.tensor(self.sj, device=dev)
+        self.K = transforms.boxcar_rows(transforms.as_morlet(None), self.dj)
         S = self.sj.size
         self.units = self.local * S * self.n
         self.bytes = self.units * 12 + self.local * self.n * 8
@@ -360,9 +362,11 @@ class C4(Workload):
 
     def step(self):
         # one fused pass: XWT power |W1 W2*|^2, phase angle and WCT coherence
+        # (transforms.wct_batch's launches: pycwt's normalisation fused into the first kernel)
         if self.local:
-            self.r = self.T.wct_batch(self.y1, self.y2, DT, self.dj, 2 * DT, -1, workspace=self.ws,
-                                      want_uv=False, want_power=True, want_phase=True)[0]
+            self.r = self.ops.wct_morlet(self.y1, self.y2, self.sjd, DT, 6.0, boxcar=self.K,
+                                         want_uv=False, want_power=True, want_phase=True,
+                                         workspace=self.ws, normalize=True)
 
     def check(self):
         """First and last pair's coherence vs the oracle's pycwt.wct (max abs difference)."""
@@ -404,6 +408,23 @@ class Stub(Workload):
 
 
 CONFIGS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5, "stub": Stub}
+# Default scaling mode per config (BASELINE.json configs): C4 ("512 series pairs ...
+# sharded by pair 1->8 GPUs") and C5 ("65536 series ... sharded across 8xMI355X") name a FIXED
+# total batch split over the GPUs -- strong scaling; C2 and C3 are single-GPU configs, so at
+# N > 1 every GPU runs the whole config on its own series -- weak scaling.
+# hipGraph replay of the step by default where it pays: strong-scaling shards of C4 are
+# launch-bound (a dozen launches + the side-stream fork / join per step)
+DEFAULT_GRAPH = {"c4": 1}
+DEFAULT_SCALING = {"c2": "weak", "c3": "weak", "c4": "strong", "c5": "strong", "stub": "weak"}
+
+
+def shard_plan(cfg, world, scaling):
+    """Every rank's rows [lo, hi) of the config under the scaling mode (no GPU touched)."""
+    from wtmi import sharding
+    B = CONFIGS[cfg].B
+    if scaling == "weak":
+        return B * world, [[r * B, (r + 1) * B] for r in range(world)]
+    return B, [list(sharding.shard_range(B, r, world)) for r in range(world)]
 CHECK_NAME = {"c2": "rank0_first_last_series_max_row_rel_err_vs_oracle",
               "c5": "rank0_last_chunk_first_last_series_max_row_rel_err_vs_oracle",
               "c3": "rank0_round_trip_max_err_rel_to_max_x",
@@ -523,9 +544,16 @@ def main():
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="keep warming up (untimed) until this many seconds have passed")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="weak: every rank its own B-row block (per-GPU work fixed); strong: the "
-                         "config's B rows split over the ranks")
+                         "config's B rows split over the ranks.  Default: strong for c4 / c5 "
+                         "(BASELINE's fixed totals sharded 1->8), weak for c2 / c3")
+    ap.add_argument("--graph", type=int, default=-1, choices=[-1, 0, 1],
+                    help="1: capture one step in a hipGraph and replay it in the timed loop; "
+                         "0: launch every step; -1 (default): per config (DEFAULT_GRAPH)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print the ranks' row ranges for --gpus / --config / --scaling as JSON "
+                         "and exit (no GPU)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--cpu-per-worker", type=int, default=0, help="0 = per-config default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -543,6 +571,13 @@ def main():
     args = ap.parse_args()
     if args.device == "cpu" and args.config != "stub":
         ap.error("--device cpu runs only --config stub")
+    if args.scaling is None:
+        args.scaling = DEFAULT_SCALING[args.config]
+    if args.plan_only:
+        total, ranges = shard_plan(args.config, args.gpus, args.scaling)
+        print(json.dumps({"config": args.config, "scaling": args.scaling, "global_batch": total,
+                          "ranks": ranges}), flush=True)
+        return 0
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout)
@@ -605,6 +640,29 @@ def main():
     barrier()
     sync()
 
+    use_graph = (DEFAULT_GRAPH.get(args.config, 0) if args.graph < 0 else args.graph) and \
+        args.device == "cuda" and wl.local > 0
+    if use_graph:
+        # one step captured (its launches, the WCT's side-stream fork / join included) and
+        # replayed: the same kernels on the same buffers, enqueued by one hipGraphLaunch
+        graph = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream(dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            wl.step()
+        torch.cuda.current_stream(dev).wait_stream(cs)
+        sync()
+        with torch.cuda.graph(graph):
+            wl.step()
+        for _ in range(max(3, args.warmup // 4)):
+            graph.replay()
+        sync()
+        step = graph.replay
+    else:
+        step = wl.step
+    barrier()
+    sync()
+
     if args.device == "cuda":
         stream = torch.cuda.current_stream(dev)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -613,13 +671,15 @@ def main():
     for i in range(args.steps):
         if args.device == "cuda":
             evs[i][0].record(stream)
-        wl.step()
+        step()
         if args.device == "cuda":
             evs[i][1].record(stream)
     sync()
+    t_own = time.perf_counter() - t0  # this rank's steps, before waiting for the others
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    t_barrier = elapsed - t_own
     if args.device == "cuda":
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     else:
@@ -629,6 +689,8 @@ def main():
     # a host tensor under gloo: wtmi.sharding)
     tmax = sharding.max_over_ranks(elapsed)
     units_all = sharding.sum_over_ranks(float(wl.units))
+    own_max, own_min = sharding.max_over_ranks(t_own), -sharding.max_over_ranks(-t_own)
+    bar_max, bar_min = sharding.max_over_ranks(t_barrier), -sharding.max_over_ranks(-t_barrier)
     check = wl.check() if rank == 0 and wl.local else None
     if want_cpu and cpu is None:  # after the timed region (default)
         cpu = cpu_baseline_child(args)
@@ -668,6 +730,12 @@ def main():
                          "per_kernel": per_kernel, "per_kernel_source": ksrc},
             "cpu_baseline": cpu,
             "check": {CHECK_NAME[args.config]: check},
+            "ranks": {"own_steps_ms_per_step": {"min": own_min / args.steps * 1e3,
+                                                "max": own_max / args.steps * 1e3},
+                      "closing_barrier_ms": {"min": bar_min * 1e3, "max": bar_max * 1e3},
+                      "note": "own = a rank's K steps up to its sync, before the closing barrier; "
+                              "value uses the max over ranks of own + barrier"},
+            "graph": bool(use_graph),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

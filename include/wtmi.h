@@ -96,6 +96,12 @@ int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long ba
                     float* out_coh, float* out_power, float* out_phase, float* out_u,
                     float* out_v, void* stream);
 
+/* Side streams the full-row WCT (n0 = 2^k >= 1024) has created in this process: it forks its
+ * full-band rows onto a side stream taken from a per-device pool and joins it before
+ * returning (on error paths too), so the count is the most such calls that ever overlapped,
+ * not the number of host threads that made one.                                     */
+long long wtmi_wct_side_streams(void);
+
 /* wtmi_wct_morlet with pycwt's own normalisation of both series, (y - mean) / std with the
  * moments in fp64 over each series (pycwt.wct / xwt normalize=True, src/wct.py:106-118), done
  * inside the transform's first kernel -- no separate moments / affine launches.  Rows of
@@ -109,9 +115,14 @@ int wtmi_wct_morlet_norm(const float* x1, const float* x2, long long ld, long lo
  * Replace the pieces of pycwt.wct_significance reached from src/wct.py:106-118 with
  * sig=True.
  * wtmi_rednoise: helpers.rednoise(n, g, 1) for `count` series into out[count][ld]:
- *   y = lfilter([1,0],[1,-g], randn(n + tau))[tau:], tau = ceil(-2/ln|g|) (0 if g == 0).
+ *   pycwt: yr = lfilter([1,0],[1,-g], randn(n + tau, 1))[tau:], tau = ceil(-2/ln|g|) (0 if
+ *   g == 0), filtered along lfilter's default axis -1 -- of length 1 -- i.e. not at all:
+ *   filtered = 0 (pycwt's literal behaviour) writes the white normals tau .. tau + n - 1;
+ *   filtered = 1 applies the AR(1) recurrence y_i = g y_{i-1} + e_i over all n + tau normals
+ *   (the MATLAB rednoise.m intent) and writes y[tau:].  |g| < 1 (-1 otherwise).
  *   Normals come from Philox4x32-10 keyed by `seed`; series c uses stream
- *   first_series + c, so batches can be drawn in pieces reproducibly.
+ *   first_series + c, so batches can be drawn in pieces reproducibly; both modes draw the
+ *   same normals.
  * wtmi_coherence_histogram: adds, for s < n_hist_scales, the counts of
  *   clamp(floor(coh[p][s][t] * nbins), 0, nbins-1) over all pairs p and
  *   t in [t_lo[s], t_hi[s]) (the points outside the cone of influence; t_lo/t_hi are
@@ -121,7 +132,7 @@ int wtmi_wct_morlet_norm(const float* x1, const float* x2, long long ld, long lo
  *   rows of hist[.][nbins]: out[s] = np.interp(level, P, (bin + 1/2) / nbins) over the
  *   non-empty bins, P = (cumsum - 1/2) / total (0 for a row without counts); out is a device
  *   float64 [n_scales].                                                              */
-int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g,
+int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g, int filtered,
                   unsigned long long seed, unsigned long long first_series, void* stream);
 int wtmi_coherence_histogram(const float* coh, long long batch, long long n0, int n_scales,
                              const int* t_lo, const int* t_hi, int n_hist_scales, int nbins,
@@ -190,9 +201,8 @@ int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batc
  * (n = 8192 / 16384 synthesis: 1 hybrid kernel with the low levels staged through LDS, 0
  * dilation chains only), wct_wide (0: windows touching a full-band row always take the
  * time-domain path; 1..3: from which union-band exponent on they take the spectral route),
- * wct_side_stream (1: the full-band rows' kernels on a per-thread side stream beside the
- * decimated rows' chain), wct_direct (1: time-path rows with s/dt <= 4.15 smoothed by direct
- * convolution instead of transforms; default 0, the transforms are faster).  The prune and kernel switches exist so that tests can
+ * wct_side_stream (1: the full-band rows' kernel on a pooled side stream beside the
+ * decimated rows' chain).  The prune and kernel switches exist so that tests can
  * compare the paths; results agree to fp32 resolution either way.  The environment gives the process
  * defaults; wtmi_set_option changes the CALLING thread's value only (thread-local), so it
  * never races a launch issued by another thread, and wtmi_get_option reads it back.

@@ -338,7 +338,7 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
         a2, _, _ = ar1(y2)
         sig = wct_significance(a1, a2, dt=dt, dj=dj, s0=s0, J=J,
                                significance_level=significance_level, wavelet=wavelet,
-                               **{k: v for k, v in kwargs.items() if k in ("mc_count", "rng")})
+                               **{k: v for k, v in kwargs.items() if k in ("mc_count", "rng", "noise")})
     else:
         sig = np.asarray([0])
     return WCT, aWCT, coi, freq, sig
@@ -350,15 +350,33 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
 # the unseeded global ``np.random``; here the generator is a parameter so tests can
 # seed it.  Parity with the GPU path is statistical (different random streams).
 
-def rednoise(N: int, g: float, a: float = 1.0, rng=None) -> np.ndarray:
-    """AR(1) red noise: lfilter([1, 0], [1, -g], randn(N + tau) * a)[tau:], with the
-    burn-in tau = ceil(-2 / ln|g|) (twice the decorrelation time); white if g == 0."""
+def rednoise(N: int, g: float, a: float = 1.0, rng=None, noise: str = "pycwt") -> np.ndarray:
+    """pycwt 0.4.0b0 ``helpers.rednoise(N, g, a)``, restated from its published source:
+
+        if g == 0: yr = np.randn(N, 1) * a          # AttributeError: numpy has no randn
+        else:
+            tau = int(np.ceil(-2 / np.log(np.abs(g))))
+            yr = lfilter([1, 0], [1, -g], np.random.randn(N + tau, 1) * a)
+            yr = yr[tau:]
+        return yr.flatten()
+
+    noise="pycwt" (default) does exactly that: scipy's lfilter filters along axis=-1, which has
+    length 1 for the (N + tau, 1) array, so the call is the identity and the noise is WHITE
+    (g only sets how many leading draws tau are dropped).  noise="red" filters along axis 0,
+    the AR(1) red noise of Grinsted's MATLAB rednoise.m (MATLAB's filter works along the first
+    non-singleton dimension), which the port meant.  DESIGN 4 records the choice; parity
+    unpinned (pycwt is absent from the image)."""
     from scipy.signal import lfilter
+    if noise not in ("pycwt", "red"):
+        raise ValueError(noise)
     rng = rng if rng is not None else np.random.default_rng()
     if g == 0:
+        if noise == "pycwt":
+            raise AttributeError("module 'numpy' has no attribute 'randn'")
         return (rng.standard_normal((N, 1)) * a).flatten()
     tau = int(np.ceil(-2 / np.log(np.abs(g))))
-    yr = lfilter([1, 0], [1, -g], rng.standard_normal((N + tau, 1)) * a, axis=0)
+    e = rng.standard_normal((N + tau, 1)) * a
+    yr = lfilter([1, 0], [1, -g], e) if noise == "pycwt" else lfilter([1, 0], [1, -g], e, axis=0)
     return yr[tau:].flatten()
 
 
@@ -407,8 +425,9 @@ def significance_from_histogram(wlc, outsidecoi, maxscale, significance_level=0.
 
 
 def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet=None,
-                     mc_count=300, rng=None, nbins=1000):
-    """pycwt ``wct_significance`` without the disk cache."""
+                     mc_count=300, rng=None, nbins=1000, noise="pycwt"):
+    """pycwt ``wct_significance`` without the disk cache; ``noise`` as in
+    ``rednoise``."""
     wavelet = wavelet or Morlet(6)
     rng = rng if rng is not None else np.random.default_rng()
     N, sj, outsidecoi, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
@@ -416,8 +435,8 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet=N
     wlc = np.zeros((J + 1, nbins))
     kw = dict(dj=dj, s0=s0, J=J, wavelet=wavelet)
     for _ in range(mc_count):
-        noise1 = rednoise(N, al1, 1, rng)
-        noise2 = rednoise(N, al2, 1, rng)
+        noise1 = rednoise(N, al1, 1, rng, noise)
+        noise2 = rednoise(N, al2, 1, rng, noise)
         nW1, sj, _, _, _, _ = cwt(noise1, dt, **kw)
         nW2, sj, _, _, _, _ = cwt(noise2, dt, **kw)
         nW12 = nW1 * nW2.conj()

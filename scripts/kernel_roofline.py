@@ -1,6 +1,6 @@
 """Per-kernel roofline of one bench config against each kernel's binding resource.
 
-Usage: python scripts/kernel_roofline.py CONFIG TRACE_DIR FETCH_DIR WRITE_DIR VALU_DIR OUT_JSON [K]
+Usage: python scripts/kernel_roofline.py CONFIG TRACE_DIR FETCH_DIR WRITE_DIR VALU_DIR OUT_JSON [K [LDS_DIR]]
 
 TRACE_DIR: `rocprofv3 --kernel-trace --stats` of `bench.py --config CONFIG` (durations: mean
 of the last K dispatches per kernel, the timed steps).  FETCH_DIR / WRITE_DIR: separate
@@ -11,7 +11,13 @@ GRBM_GUI_ACTIVE` pass.  Per kernel (PMC values: mean per dispatch after the firs
   valu_busy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
               (quad-cycles with a VALU instruction issuing, summed over waves, over the SIMD
               cycles of the dispatch: GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles)
-  bound     = whichever fraction is larger; frac = that fraction.
+  lds_busy  = SQ_LDS_IDX_ACTIVE x 8 / (256 CUs x GRBM_GUI_ACTIVE) (LDS-array cycles per CU cycle),
+              from an optional LDS_DIR pass `--pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT
+              SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE`; with it
+              lds_conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (share of LDS cycles lost
+              to bank conflicts) and lds_issue_wait = SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES (share of
+              wave cycles stalled issuing an LDS instruction)
+  bound     = whichever of hbm / valu / lds is largest; frac = that fraction.
 OUT_JSON is updated in place (one entry per config).
 """
 import csv
@@ -68,8 +74,10 @@ def counters(d):
 def main():
     cfg, tdir, fdir, wdir, vdir, out = sys.argv[1:7]
     k = int(sys.argv[7]) if len(sys.argv) > 7 else 10
+    ldir = sys.argv[8] if len(sys.argv) > 8 else None
     dur = durations(tdir, k)
     fetch, write, valu = counters(fdir), counters(wdir), counters(vdir)
+    lds = counters(ldir) if ldir else {}
     rows = []
     for name, ms in sorted(dur.items(), key=lambda kv: -kv[1]):
         if not name.startswith("wtmi::"):
@@ -81,12 +89,25 @@ def main():
         grbm = v.get("GRBM_GUI_ACTIVE", 0.0)
         busy = v.get("SQ_ACTIVE_INST_VALU", 0.0) * 4.0 / (SIMDS * grbm / 8.0) if grbm else None
         hf = gbs / HBM_PEAK_GBS
-        bound = "valu" if busy is not None and busy > hf else "hbm"
-        rows.append({"kernel": name, "ms": round(ms, 4), "hbm_bytes": round(hbm),
-                     "hbm_GBps": round(gbs, 1), "hbm_frac": round(hf, 3),
-                     "valu_busy": None if busy is None else round(busy, 3),
-                     "valu_insts": v.get("SQ_INSTS_VALU"),
-                     "bound": bound, "frac": round(max(hf, busy or 0.0), 3)})
+        L = lds.get(name, {})
+        lg = L.get("GRBM_GUI_ACTIVE", 0.0)
+        lbusy = L["SQ_LDS_IDX_ACTIVE"] * 8.0 / (256 * lg) if lg and "SQ_LDS_IDX_ACTIVE" in L else None
+        lconf = (L.get("SQ_LDS_BANK_CONFLICT", 0.0) / L["SQ_LDS_IDX_ACTIVE"]
+                 if L.get("SQ_LDS_IDX_ACTIVE") else None)
+        lwait = (L.get("SQ_WAIT_INST_LDS", 0.0) / L["SQ_WAVE_CYCLES"] if L.get("SQ_WAVE_CYCLES") else None)
+        fr = {"hbm": hf, "valu": busy or 0.0, "lds": lbusy or 0.0}
+        bound = max(fr, key=fr.get)
+        row = {"kernel": name, "ms": round(ms, 4), "hbm_bytes": round(hbm),
+               "hbm_GBps": round(gbs, 1), "hbm_frac": round(hf, 3),
+               "valu_busy": None if busy is None else round(busy, 3),
+               "valu_insts": v.get("SQ_INSTS_VALU"),
+               "bound": bound, "frac": round(fr[bound], 3)}
+        if ldir:
+            row.update(lds_busy=None if lbusy is None else round(lbusy, 3),
+                       lds_conflict=None if lconf is None else round(lconf, 3),
+                       lds_issue_wait=None if lwait is None else round(lwait, 3),
+                       lds_insts=L.get("SQ_INSTS_LDS"))
+        rows.append(row)
     data = {}
     if os.path.exists(out):
         with open(out) as fh:
@@ -96,7 +117,8 @@ def main():
         json.dump(data, fh, indent=1)
     for r in rows:
         print(f"{r['ms']:8.4f} ms  {r['bound']:4s} frac {r['frac']:.3f}  hbm {r['hbm_GBps']:7.1f} GB/s  "
-              f"valu {r['valu_busy']}  {r['kernel']}")
+              f"valu {r['valu_busy']}  lds {r.get('lds_busy')} conf {r.get('lds_conflict')} "
+              f"ldswait {r.get('lds_issue_wait')}  {r['kernel']}")
 
 
 if __name__ == "__main__":

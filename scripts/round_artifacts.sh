@@ -5,11 +5,12 @@
 #   2. rocprofv3 --kernel-trace --stats per config   -> gpurun_out/prof_<cfg>/
 #   3. bench.py per config (CPU baseline included)   -> gpurun_out/bench_<cfg>.json
 #   4. (r03) a VALU PMC pass per config + the traces -> gpurun_out/kernel_roofline.json
-#      (per-kernel binding resource; copied into profiles/$ROUND/ like pmc_traffic.json)
+#      (per-kernel binding resource; copied into profiles/$ROUND/ like pmc_traffic.json);
+#      (r04) plus an LDS pass (array cycles, bank conflicts, LDS issue stalls)
 #   PARTS selects the parts: "pmc prof roof bench" (default all).
 # Every GPU step has its own time limit; a crash / abort / timeout ends the session.
 set -u
-ROUND=${ROUND:-r03}
+ROUND=${ROUND:-r04}
 PARTS=${PARTS:-"pmc prof roof bench"}
 CFGS=${CFGS:-"c2 c3 c4 c5"}
 OUT=gpurun_out
@@ -43,10 +44,17 @@ if has prof; then
 fi
 if has roof; then
   for c in $CFGS; do
+    TR=$OUT/prof_$c
+    if [ $c = c4 ]; then  # per-kernel durations from a one-stream trace (each kernel's own time)
+      WTMI_WCT_SIDE_STREAM=0 run prof_c4_serial 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4_serial -o run -- python bench.py --config c4 --steps 10 --warmup 5 --no-cpu-baseline
+      python scripts/trace_mean.py $OUT/prof_c4_serial 10 > $OUT/prof_c4_serial/timed_mean.txt
+      TR=$OUT/prof_c4_serial
+    fi
     run valu_$c 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/valu_$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
+    run lds_$c 400 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/lds_$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
     STEPS_K=10
     [ $c = c2 ] && STEPS_K=50
-    python scripts/kernel_roofline.py $c $OUT/prof_$c $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/valu_$c $OUT/kernel_roofline.json $STEPS_K > $OUT/roof_$c.txt || exit 1
+    python scripts/kernel_roofline.py $c $TR $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/valu_$c $OUT/kernel_roofline.json $STEPS_K $OUT/lds_$c > $OUT/roof_$c.txt || exit 1
     head -4 $OUT/roof_$c.txt
   done
   cp $OUT/kernel_roofline.json profiles/$ROUND/kernel_roofline.json

@@ -1,4 +1,4 @@
-"""bench.py's multi-rank launcher, weak (default) and strong scaling, on CPU (gloo, stub workload).
+"""bench.py's multi-rank launcher, weak and strong scaling, on CPU (gloo, stub workload).
 
 `python bench.py --gpus N` must start N ranks itself when no torch.distributed.run
 environment is present, give each rank its own block (weak: B rows per rank; strong: the
@@ -41,7 +41,7 @@ def test_gpus_flag_launches_that_many_ranks_strong(n, per_rank):
 
 
 @pytest.mark.parametrize("n", [1, 2, 3])
-def test_weak_scaling_is_the_default_one_block_per_rank(n):
+def test_weak_scaling_is_the_stub_default_one_block_per_rank(n):
     r, d = _run("--gpus", str(n))
     assert r.returncode == 0, r.stderr[-2000:]
     assert d["n_gpus"] == n and d["scaling"] == "weak"
@@ -79,3 +79,40 @@ def test_cpu_baseline_child_prints_one_record():
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["cores"] == 1 and rec["kind"] == "port" and rec["unit"] == "coeffs/s"
     assert rec["value"] > 0 and "sample" in rec and "cpu_model" in rec
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("cfg,total", [("c4", 512), ("c5", 65536)])
+def test_fixed_total_configs_default_to_strong_scaling(cfg, total, n):
+    """BASELINE configs[3] (512 pairs "sharded by pair 1->8 GPUs") and configs[4] (65536
+    series "sharded across 8xMI355X") are fixed totals: under the default scaling the ranks'
+    blocks tile exactly [0, total) -- contiguous, disjoint, whatever N."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--gpus", str(n),
+                        "--plan-only"], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["scaling"] == "strong" and d["global_batch"] == total
+    assert len(d["ranks"]) == n
+    assert d["ranks"][0][0] == 0 and d["ranks"][-1][1] == total
+    for (a, b), (c, _) in zip(d["ranks"], d["ranks"][1:]):
+        assert b == c and a <= b
+
+
+@pytest.mark.parametrize("cfg,per", [("c2", 1024), ("c3", 8192)])
+def test_single_gpu_configs_default_to_weak_scaling(cfg, per):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--gpus", "4",
+                        "--plan-only"], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["scaling"] == "weak" and d["global_batch"] == 4 * per
+    assert d["ranks"] == [[k * per, (k + 1) * per] for k in range(4)]
+
+
+def test_per_rank_timing_fields():
+    r, d = _run("--gpus", "2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    rk = d["ranks"]
+    assert 0 <= rk["own_steps_ms_per_step"]["min"] <= rk["own_steps_ms_per_step"]["max"]
+    assert 0 <= rk["closing_barrier_ms"]["min"] <= rk["closing_barrier_ms"]["max"]
+    assert rk["own_steps_ms_per_step"]["max"] <= d["ms_per_step"] * 1.0001
+    assert d["graph"] is False

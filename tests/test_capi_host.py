@@ -34,8 +34,21 @@ def test_prototype_arity_matches_header():
     for name, (_, args) in _lib.PROTOTYPES.items():
         m = re.search(name + r"\s*\(([^;]*)\)\s*;", txt, flags=re.S)
         assert m, name
-        nargs = len([a for a in m.group(1).split(",") if a.strip()])
+        nargs = len([a for a in m.group(1).split(",") if a.strip() and a.strip() != "void"])
         assert nargs == len(args), (name, nargs, len(args))
+
+
+def test_integration_table_lists_every_header_symbol():
+    """INTEGRATION.md section 2's C-ABI table names every entry point include/wtmi.h declares,
+    each in a row that says what reference call it replaces."""
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    table = txt[txt.index("| C entry point |"):]
+    table = table[:table.index("\n\n")]
+    rows = [r for r in table.splitlines()[2:] if r.startswith("|")]
+    for name in header_functions():
+        hit = [r for r in rows if re.search(r"`" + name + r"`", r.split("|")[1])]
+        assert hit, name
+        assert len(hit[0].split("|")[2].strip()) > 10, name
 
 
 def test_invalid_arguments_rejected_without_gpu():
@@ -79,7 +92,8 @@ def test_empty_batch_is_a_noop_without_gpu():
     assert lib.wtmi_series_moments(N, 0, 16, 0, 16, N, N) == 0
     assert lib.wtmi_series_affine(N, 0, 16, 0, 16, 1, N, N, N) == 0
     assert lib.wtmi_affine(N, 0, 16, 0, 16, N, N, 0, 16, N) == 0
-    assert lib.wtmi_rednoise(N, 16, 0, 16, 0.5, 1, 0, N) == 0
+    assert lib.wtmi_rednoise(N, 16, 0, 16, 0.5, 0, 1, 0, N) == 0
+    assert lib.wtmi_rednoise(N, 16, 0, 16, 0.5, 2, 1, 0, N) == -1  # filtered is 0 or 1
     assert lib.wtmi_coherence_histogram(N, 0, 16, 4, N, N, 4, 1000, N, N) == 0
     assert lib.wtmi_coherence_quantile(N, 0, 1000, 0.95, N, N) == 0
     # sizes are still validated first, and a non-empty batch still needs its arrays

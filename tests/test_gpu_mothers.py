@@ -62,16 +62,23 @@ def test_run_cwt_other_mothers(mother):
 
 @pytest.mark.parametrize("key", ["paul", "DOG", "mexicanhat"])
 def test_run_xwt_other_mothers(key):
-    """src.xwt.run_xwt with MOTHER_DICT[key]: power and significance ratio as pycwt.xwt +
-    normalize_xwt_results; phase arrows from angle(W1 W2*) at dj = 1/12 (what pycwt.wct
-    returns as aWCT -- the reference itself fails in pycwt.wct there, no Paul/DOG smooth)."""
+    """src.xwt.run_xwt with MOTHER_DICT[key] raises AttributeError, as the reference does in
+    pycwt.wct (no Paul/DOG smooth), before any launch.  The engine's explicit alternative,
+    run_xwt_batch(..., phase_without_smooth=True): power and significance ratio as pycwt.xwt
+    + normalize_xwt_results; phase arrows from angle(W1 W2*) at dj = 1/12 (what pycwt.wct
+    returns as aWCT)."""
     import src.xwt as xwt
     rng = np.random.default_rng(8)
     y1 = red_series(rng, 900).astype(np.float64)
     y2 = 0.6 * np.roll(y1, 4) + 0.8 * red_series(rng, 900)
     m = xwt.MOTHER_DICT[key]
     om = {"paul": pc.Paul(4), "DOG": pc.DOG(2), "mexicanhat": pc.MexicanHat()}[key]
-    r = xwt.run_xwt(xwt.DataForXWT(y1, y2, m, xwt.DT, xwt.DJ, xwt.S0, xwt.LEVELS))
+    data = xwt.DataForXWT(y1, y2, m, xwt.DT, xwt.DJ, xwt.S0, xwt.LEVELS)
+    with pytest.raises(AttributeError, match="smooth"):
+        xwt.run_xwt(data)
+    with pytest.raises(AttributeError, match="smooth"):
+        xwt.run_xwt_batch([data])
+    r = xwt.run_xwt_batch([data], phase_without_smooth=True)[0]
     W12, coi, freqs, signif = pc.xwt(y1, y2, dt=xwt.DT, dj=xwt.DJ, s0=xwt.S0, wavelet=om)
     period, power, sig95, coi_plot = gs.normalize_xwt_results(
         y1.size, W12, coi, np.log2(xwt.LEVELS[2]), freqs, signif)

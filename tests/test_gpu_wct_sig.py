@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 def test_rednoise_ar1_statistics_and_streams():
     from wtmi import ops
     g, n = 0.7, 16384
-    x = ops.rednoise(256, n, g, seed=123).double().cpu().numpy()
+    x = ops.rednoise(256, n, g, seed=123, noise="red").double().cpu().numpy()
     r1 = np.mean([np.corrcoef(r[:-1], r[1:])[0, 1] for r in x])
     assert abs(r1 - g) < 0.005, r1
     assert abs(x.var() - 1 / (1 - g * g)) < 0.03 * (1 / (1 - g * g)), x.var()
@@ -29,12 +29,32 @@ def test_rednoise_ar1_statistics_and_streams():
     # stationary from the first sample on (the tau burn-in is dropped)
     assert abs(x[:, 0].var() / (1 / (1 - g * g)) - 1) < 0.25
     # counter-based streams: same (seed, series) -> same draws; different -> different
-    y = ops.rednoise(4, n, g, seed=123, first_series=2).cpu().numpy()
+    y = ops.rednoise(4, n, g, seed=123, first_series=2, noise="red").cpu().numpy()
     np.testing.assert_array_equal(y[:2], x[2:4].astype(np.float32))
-    z = ops.rednoise(2, n, g, seed=124).cpu().numpy()
+    z = ops.rednoise(2, n, g, seed=124, noise="red").cpu().numpy()
     assert not np.allclose(z, x[:2])
-    w = ops.rednoise(64, 4096, 0.0, seed=9).double().cpu().numpy()  # white
+    w = ops.rednoise(64, 4096, 0.0, seed=9, noise="red").double().cpu().numpy()  # g = 0: white
     assert abs(np.mean([np.corrcoef(r[:-1], r[1:])[0, 1] for r in w])) < 0.01
+
+
+@pytest.mark.parametrize("g", [0.7, 0.98, -0.4])
+def test_rednoise_pycwt_mode_is_white_and_shares_the_normals(g):
+    """noise="pycwt" (the default): pycwt's lfilter along the length-1 axis leaves
+    randn(N + tau, 1) unfiltered, so rows are white N(0, 1) -- lag-1 correlation ~ 0 whatever
+    g -- and they are the very normals the red mode filters: red[i] - g red[i-1] = white[i]."""
+    from wtmi import ops
+    n, count = 8192, 128
+    w = ops.rednoise(count, n, g, seed=7).double().cpu().numpy()
+    r1 = np.mean([np.corrcoef(r[:-1], r[1:])[0, 1] for r in w])
+    assert abs(r1) < 4 / np.sqrt(n * count), r1
+    assert abs(w.var() - 1.0) < 0.02, w.var()
+    assert abs(w.mean()) < 0.01
+    red = ops.rednoise(count, n, g, seed=7, noise="red").double().cpu().numpy()
+    innov = red[:, 1:] - g * red[:, :-1]
+    scale = max(1.0, 1 / np.sqrt(1 - g * g))
+    assert np.abs(innov - w[:, 1:]).max() < 2e-6 * scale * 8
+    with pytest.raises(ValueError):
+        ops.rednoise(2, 16, g, seed=1, noise="blue")
 
 
 @pytest.mark.parametrize("B,S,n0,nh", [(3, 7, 500, 5), (64, 13, 96, 12), (1, 1, 1, 1)])
@@ -59,11 +79,12 @@ def test_coherence_histogram_exact(B, S, n0, nh):
     np.testing.assert_array_equal(got, ref.astype(np.uint32))
 
 
-def test_wct_significance_matches_oracle_monte_carlo():
+@pytest.mark.parametrize("noise", ["pycwt", "red"])
+def test_wct_significance_matches_oracle_monte_carlo(noise):
     from wtmi import transforms
     args = (0.5, 0.3, 1.0, 0.25, 2.0, 12)
-    got = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=False)
-    refs = np.array([pc.wct_significance(*args, mc_count=300, rng=np.random.default_rng(i))
+    got = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=False, noise=noise)
+    refs = np.array([pc.wct_significance(*args, mc_count=300, rng=np.random.default_rng(i), noise=noise)
                      for i in range(3)])
     ref = refs.mean(axis=0)
     np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
@@ -71,10 +92,30 @@ def test_wct_significance_matches_oracle_monte_carlo():
     d = np.abs(got[ok] - ref[ok])
     assert d.max() < 0.06, (got, ref)
     assert d.mean() < 0.025, (got, ref)
-    # reproducible for a fixed seed, and cached per argument set
-    again = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True)
+    # reproducible for a fixed seed, and cached per argument set (the noise mode is in the key)
+    again = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True, noise=noise)
     np.testing.assert_array_equal(again, got)
-    assert transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True) is not again
+    assert transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True, noise=noise) is not again
+
+
+def test_wct_significance_noise_modes_and_g0_raises():
+    """The two readings on a strongly red pair (g = 0.98, the app's inflation.csv regime) with
+    the same seed: different noise, hence different levels, but close -- the coherence of
+    independent noise depends little on its spectrum (oracle, 60 passes: max difference 0.029
+    between the modes against 0.058 between two seeds of one mode).  The default is pycwt's
+    literal (white) reading; g == 0 raises AttributeError as pycwt's rednoise does (np.randn)."""
+    from wtmi import transforms
+    args = (0.98, 0.98, 1 / 12, 1 / 8, 2 / 12, 56)
+    white = transforms.wct_significance(*args, mc_count=100, seed=5, cache=False)
+    red = transforms.wct_significance(*args, mc_count=100, seed=5, cache=False, noise="red")
+    ok = np.isfinite(white) & np.isfinite(red)
+    np.testing.assert_array_equal(ok, np.isfinite(white))
+    assert ok.sum() > 10
+    assert not np.array_equal(white[ok], red[ok])
+    assert np.abs(white[ok] - red[ok]).max() < 0.1
+    assert transforms.SIG_NOISE == "pycwt"
+    with pytest.raises(AttributeError):
+        transforms.wct_significance(0.0, 0.5, 1.0, 0.25, 2.0, 12, mc_count=2, cache=False)
 
 
 def test_run_wct_with_significance_app_shape():

@@ -51,11 +51,27 @@ def test_oracle_counter_clamps_and_counts():
     assert wlc[1].sum() == 0  # s = maxscale is not counted
 
 
-def test_oracle_rednoise_is_ar1():
-    x = pc.rednoise(200000, 0.7, 1.0, np.random.default_rng(1))
+def test_oracle_rednoise_modes():
+    """noise="red": AR(1) with lag-1 correlation g and variance 1/(1-g^2).  noise="pycwt"
+    (the default, pycwt's published rednoise taken literally): lfilter along the length-1
+    axis of randn(N + tau, 1) is the identity, so the draws are white -- exactly the normals
+    after the tau burn-in of the same generator state -- and g == 0 raises AttributeError
+    (pycwt's np.randn)."""
+    x = pc.rednoise(200000, 0.7, 1.0, np.random.default_rng(1), noise="red")
     r1 = np.corrcoef(x[:-1], x[1:])[0, 1]
     assert abs(r1 - 0.7) < 0.01
     assert abs(x.var() - 1 / (1 - 0.49)) < 0.05
+    w = pc.rednoise(200000, 0.7, 1.0, np.random.default_rng(1))
+    assert abs(np.corrcoef(w[:-1], w[1:])[0, 1]) < 0.01
+    assert abs(w.var() - 1.0) < 0.02
+    tau = int(np.ceil(-2 / np.log(0.7)))
+    e = np.random.default_rng(1).standard_normal((200000 + tau, 1)).flatten()
+    np.testing.assert_array_equal(w, e[tau:])
+    # the red series is the AR(1) filter of those same normals
+    np.testing.assert_allclose(x[1:] - 0.7 * x[:-1], e[tau + 1:], atol=1e-9)
+    with pytest.raises(AttributeError):
+        pc.rednoise(100, 0.0, 1.0, np.random.default_rng(1))
+    assert pc.rednoise(100, 0.0, 1.0, np.random.default_rng(1), noise="red").shape == (100,)
 
 
 def test_quantile_known_answer_with_empty_bins_at_the_crossing():

@@ -113,8 +113,9 @@ __device__ __forceinline__ cpx fast_atan2f_x2(cpx y, cpx x) {
 // pairs (which the FFT kernels otherwise keep live across the scale loop).  The
 // pointer must be wave-uniform; readfirstlane makes that provable to the compiler.
 // bytes: the descriptor's extent; accesses past it are dropped (stores) or read 0 (loads) by
-// the hardware range check -- a padded row (n0 < N) passes n0 * sizeof(T) and stores its 16
-// positions per thread without per-lane branches.
+// the hardware range check.  Callers that rely on it put the out-of-range offset in voffset
+// (e.g. voffset = extent), never only in soffset: whether the range check counts the SGPR
+// offset is not something this code assumes (put_row, store_row, band_load).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes = 0x7fffffff) {
   const unsigned long long u = reinterpret_cast<unsigned long long>(p);
   const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(u));
@@ -171,10 +172,6 @@ struct Options {
                             // from e >= wct_wide (1..3); 0 = never (time path)
   int wct_side_stream = 1;  // WTMI_WCT_SIDE_STREAM: full-band rows on a side stream beside the
                             // decimated rows' chain (1), or all on the caller's stream (0)
-  int wct_direct = 0;       // WTMI_WCT_DIRECT: time smoothing of the narrow-Gaussian time-path rows
-                            // (s/dt <= 4.15) by direct convolution in their own kernel (1), or by
-                            // transforms with the other full-band rows (0, default: faster on
-                            // MI355X at every measured size)
 };
 const Options& options();
 

@@ -31,8 +31,9 @@ __device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, 
   float* pu_ = (KIND & kOutUV) ? a.out_u + rowbase : nullptr;
   float* pv_ = (KIND & kOutUV) ? a.out_v + rowbase : nullptr;
   // Rows whose owner is a whole wave (NT >= 64 -> the row, hence rowbase, is wave-uniform)
-  // go through buffer stores: SGPR row base + one voffset VGPR; a padded row's positions
-  // past n0 fall outside the descriptor's extent and are dropped by the hardware.
+  // go through buffer stores: SGPR row base + one voffset VGPR.  A padded row's positions
+  // past n0 get voffset = the extent itself, so the range check drops them whether or not it
+  // counts the SGPR offset (wct.hip put_row).
   constexpr bool kBuf = P::NT >= kWave;
   if constexpr (kBuf) {
     __amdgpu_buffer_rsrc_t rw, rp, rs, ru, rv;
@@ -44,18 +45,20 @@ __device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, 
       ru = uniform_rsrc(pu_, n4);
       rv = uniform_rsrc(pv_, n4);
     }
+    auto vo = [&](int m, int sz) { return (FULL || t + m * P::NT < a.n0) ? sz * t : sz * a.n0; };
 #pragma unroll
     for (int m = 0; m < 16; ++m)
-      if constexpr (KIND & kOutW) buf_st(v[m], rw, 8 * t, 8 * m * P::NT);
+      if constexpr (KIND & kOutW) buf_st(v[m], rw, vo(m, 8), 8 * m * P::NT);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const float pw = cabs2(v[m]);
-      if constexpr (KIND & kOutPow) buf_st(pw, rp, 4 * t, 4 * m * P::NT);
-      if constexpr (KIND & kOutSig) buf_st(pw * sg, rs, 4 * t, 4 * m * P::NT);
+      const int o4 = vo(m, 4);
+      if constexpr (KIND & kOutPow) buf_st(pw, rp, o4, 4 * m * P::NT);
+      if constexpr (KIND & kOutSig) buf_st(pw * sg, rs, o4, 4 * m * P::NT);
       if constexpr (KIND & kOutUV) {
         const float r = sqrtf(pw);
-        buf_st(r > 0.f ? v[m].y / r : 0.f, ru, 4 * t, 4 * m * P::NT);
-        buf_st(r > 0.f ? v[m].x / r : 1.f, rv, 4 * t, 4 * m * P::NT);
+        buf_st(r > 0.f ? v[m].y / r : 0.f, ru, o4, 4 * m * P::NT);
+        buf_st(r > 0.f ? v[m].x / r : 1.f, rv, o4, 4 * m * P::NT);
       }
     }
     return;

@@ -39,6 +39,8 @@ struct CwtArgs {
                          // xwt / wct), in place of the affine pointers
 };
 
+inline namespace WTMI_FFT_NS {
+
 // Filter constants of a mother wavelet (pycwt 0.4.0b0 mothers.py: Paul.psi_ft, DOG.psi_ft).
 inline bool mother_consts(CwtArgs& a, int mother, double param) {
   a.mother = mother;
@@ -349,4 +351,5 @@ __device__ __forceinline__ cpx morlet_bin0(cpx X0, cpx prm, float f0, int t) {
   return cscale(X0, __builtin_amdgcn_exp2f(fmaf(e * K, e, prm.y)));
 }
 
+}  // inline namespace WTMI_FFT_NS
 }  // namespace wtmi

@@ -19,7 +19,25 @@
 
 #include "common.hpp"
 
+// Twiddle products: cmul2 / cmul2_conj (two packed instructions each, common.hpp) unless the
+// translation unit defines WTMI_PK_TWIDDLES 0 before including this header.  The asm
+// products cut the WCT kernels' VALU by 5-9 % (C4 3.27 -> 3.1 ms) but cost the store-bound
+// CWT kernel ~1 % (0.792 -> 0.804 ms per C2 launch, A/B on one box; the hazard recognizer
+// pads each asm result's first reader with an s_nop), so cwt.hip keeps the plain products.
+// Everything that depends on the choice (this header and cwt_common.hpp's kernels' pieces)
+// sits in an inline namespace named after it, so the two variants are distinct entities
+// (no same-named inline function with two bodies across translation units).
+#ifndef WTMI_PK_TWIDDLES
+#define WTMI_PK_TWIDDLES 1
+#endif
+#if WTMI_PK_TWIDDLES
+#define WTMI_FFT_NS fft_pk
+#else
+#define WTMI_FFT_NS fft_plain
+#endif
+
 namespace wtmi {
+inline namespace WTMI_FFT_NS {
 
 // cos / sin of 2*pi*m/16
 __host__ __device__ constexpr float cos16(int m) {
@@ -330,14 +348,6 @@ __device__ __forceinline__ cpx opaque(cpx w) {
   return w;
 }
 
-// Twiddle products: cmul2 / cmul2_conj (two packed instructions each, common.hpp) unless the
-// translation unit defines WTMI_PK_TWIDDLES 0 before including this header.  The asm
-// products cut the WCT kernels' VALU by 5-9 % (C4 3.27 -> 3.1 ms) but cost the store-bound
-// CWT kernel ~1 % (0.792 -> 0.804 ms per C2 launch, A/B on one box; the hazard recognizer
-// pads each asm result's first reader with an s_nop), so cwt.hip keeps the plain products.
-#ifndef WTMI_PK_TWIDDLES
-#define WTMI_PK_TWIDDLES 1
-#endif
 constexpr bool kPkTwiddles = WTMI_PK_TWIDDLES != 0;
 
 // (plain products) v[r] *= w^r for r = 1..NZ-1 from the bases w, w^2, w^4, w^8 (inputs r >= NZ are zero
@@ -628,4 +638,5 @@ __device__ __forceinline__ void band_entry(cpx (&v)[16], cpx y, cpx* __restrict_
   for (int r = 0; r < 16; ++r) v[r] = r < NZ ? lds[base + r * STEP] : mkc(0.f, 0.f);
 }
 
+}  // inline namespace WTMI_FFT_NS
 }  // namespace wtmi

@@ -22,7 +22,6 @@ constexpr Entry kEntries[] = {
     {"modwt_syn", &Options::modwt_syn, 0, 1},
     {"wct_wide", &Options::wct_wide, 0, 4},
     {"wct_side_stream", &Options::wct_side_stream, 0, 1},
-    {"wct_direct", &Options::wct_direct, 0, 1},
 };
 
 // Process defaults: the environment, read once (immutable afterwards).
@@ -58,7 +57,7 @@ const Options& options() { return thread_options(); }
 }  // namespace wtmi
 
 // Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
-// wct_min_rows, wct_dec_rows, modwt_syn, wct_wide, wct_side_stream, wct_direct) for the CALLING
+// wct_min_rows, wct_dec_rows, modwt_syn, wct_wide, wct_side_stream) for the CALLING
 // thread.  0 on success, -1 unknown
 // name or out of range.  Applies to launches this thread issues after the call; other
 // threads keep their own values (the process defaults come from WTMI_<NAME>).

@@ -22,6 +22,10 @@
 // (wct_dec_kernel) and band inverses of M bins here.
 // Phase B (one thread = one time column of one pair): streams the time-path rows of T
 // once, keeps the last K rows in registers and writes WCT.
+#include <atomic>
+#include <mutex>
+#include <vector>
+
 #include "cwt_common.hpp"
 #include "long_path.hpp"
 
@@ -115,16 +119,28 @@ __device__ __forceinline__ void load_spec(cpx (&X)[16], const cpx* row, int t) {
 }
 
 // Row store of 16 positions per thread.  BUF (rows owned by whole waves): buffer stores off
-// a wave-uniform row base, no per-position address registers, the descriptor's extent
-// n0 * sizeof(T) dropping the positions past a padded row's end; otherwise plain stores
-// masked to pos < n0.
-template <int LOGN, bool BUF, typename T, typename F>
+// a wave-uniform row base, no per-position address registers; otherwise plain stores
+// masked to pos < n0.  A padded row (n0 < N) sends the positions past
+// n0 to voffset = n0 * sizeof(T), outside the descriptor's extent whether or not the
+// hardware's range check counts the SGPR offset (the position's m * NT part sits there), so
+// they are dropped and never reach the next row or past the buffer's end.
+// FULL: the full-row kernels (n0 = N) compile only the unmasked loop, the padded-row kernels
+// (launched for n0 < N) only the masked one -- a runtime choice between two copies of the
+// store loop cost phase A registers (48 -> 140 spilled bytes per lane).
+template <int LOGN, bool BUF, bool FULL, typename T, typename F>
 __device__ __forceinline__ void put_row(T* row, int t, int n0, F&& val) {
   using P = FftPlan<LOGN>;
   if constexpr (BUF) {
-    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row, n0 * static_cast<int>(sizeof(T)));
+    constexpr int SZ = static_cast<int>(sizeof(T));
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row, n0 * SZ);
+    if constexpr (FULL) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) buf_st(val(m), r, static_cast<int>(sizeof(T)) * t, static_cast<int>(sizeof(T)) * m * P::NT);
+      for (int m = 0; m < 16; ++m) buf_st(val(m), r, SZ * t, SZ * m * P::NT);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        buf_st(val(m), r, t + m * P::NT < n0 ? SZ * t : SZ * n0, SZ * m * P::NT);
+    }
   } else {
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
@@ -232,23 +248,23 @@ __device__ __forceinline__ int wct_regime(double s, double dt, double f0, double
 }
 
 // Per-row outputs of the XWT shape from W12 (|W12|^2, angle, arrows).
-template <int LOGN, bool BUF>
+template <int LOGN, bool BUF, bool FULL>
 __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16], long long rowbase, int t) {
   const int n0 = a.n0;
-  if (a.out_pow) put_row<LOGN, BUF>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w[m]); });
+  if (a.out_pow) put_row<LOGN, BUF, FULL>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w[m]); });
   if (a.out_sig) {  // phase angle, two positions per packed polynomial
     cpx ang[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m)
       ang[m] = fast_atan2f_x2(cpx{w[2 * m].y, w[2 * m + 1].y}, cpx{w[2 * m].x, w[2 * m + 1].x});
-    put_row<LOGN, BUF>(a.out_sig + rowbase, t, n0, [&](int m) { return ang[m >> 1][m & 1]; });
+    put_row<LOGN, BUF, FULL>(a.out_sig + rowbase, t, n0, [&](int m) { return ang[m >> 1][m & 1]; });
   }
   if (a.out_u) {
-    put_row<LOGN, BUF>(a.out_u + rowbase, t, n0, [&](int m) {
+    put_row<LOGN, BUF, FULL>(a.out_u + rowbase, t, n0, [&](int m) {
       const float r = sqrtf(cabs2(w[m]));
       return r > 0.f ? w[m].y / r : 0.f;
     });
-    put_row<LOGN, BUF>(a.out_v + rowbase, t, n0, [&](int m) {
+    put_row<LOGN, BUF, FULL>(a.out_v + rowbase, t, n0, [&](int m) {
       const float r = sqrtf(cabs2(w[m]));
       return r > 0.f ? w[m].x / r : 1.f;
     });
@@ -274,25 +290,11 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
 //                   (eu in 1..3: the window holds rows of regime q = 0 but none of band ew = 0),
 //                   its coherence comes from the WB spectra through one band inverse of Mu bins
 //                   per field instead of the time-domain workspace
-//   bit 18    direct time-path row (needT only, q = 0, not decimated) whose time Gaussian is narrow
-//                   (sigma = s/dt <= kDirectMaxSigma samples): smoothed by direct convolution with
-//                   the sampled Gaussian in phase A's kind-3 kernel instead of two transforms a field
 enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5,
-             kPlanNeedW = 128, kPlanDecShift = 8, kPlanEwShift = 12, kPlanEuShift = 16,
-             kPlanDirect = 1 << 18 };
+             kPlanNeedW = 128, kPlanDecShift = 8, kPlanEwShift = 12, kPlanEuShift = 16 };
 __device__ __forceinline__ int plan_dec(int pl) { return (pl >> kPlanDecShift) & 15; }
 __device__ __forceinline__ int plan_ew(int pl) { return (pl >> kPlanEwShift) & 15; }
 __device__ __forceinline__ int plan_eu(int pl) { return (pl >> kPlanEuShift) & 3; }
-// Direct smoothing (kPlanDirect): sigma <= 4.15 samples, taps |d| <= R with R + 1 >= kBandT sigma
-// (the dropped taps are below exp(-kBandT^2/2) = 6.8e-10 of the centre one, the criterion the
-// spectral routes use for the Gaussian's band); tap classes R = 18 (sigma <= 2.92) and R = 26;
-// rows of 1024 <= N <= 8192 (NT >= 64: a wave holds one row's taps, the halo fits the m = 0 / 15
-// slots)
-constexpr double kDirectMaxSigma = 4.15;
-constexpr int kDirectMinLogn = 10;
-constexpr int kDirectMaxLogn = 13;  // N = 16384: 1024-thread workgroups, 128 VGPRs, spills
-constexpr int kDirectR0 = 18, kDirectR1 = 26;
-constexpr int kDirectHalo = 32;
 // wide windows need M = N >> 3 >= 32 bins (one band phasor per thread): LOGN >= 8; the
 // spectral boxcar keeps K rows in registers: K <= 24
 constexpr int kWideMinLogn = 8;
@@ -351,7 +353,7 @@ __device__ __forceinline__ int plan_q(const double* scales, int r, double dt, do
 // decimated rows' list (S ints) and schedule (kDecSched ints), see wct_dec_kernel.
 template <int LOGN>
 __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales, int S, double dt, double f0,
-                                              int K, int prune, int dec, int wide, int direct,
+                                              int K, int prune, int dec, int wide,
                                               long long batch, int* __restrict__ plan,
                                               int* __restrict__ scratch) {
   __shared__ int last;
@@ -391,10 +393,7 @@ __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales,
       else needT = true;
     }
     const int qw = qwin[r] & 15, eu = (qwin[r] >> 4) & 3;
-    const bool dir = direct && prune && LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn && q == 0 &&
-                     e == 0 && needT && !needS && !needW && scales[r] / dt <= kDirectMaxSigma;
     plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
-              (dir ? kPlanDirect : 0) |
               (needW ? kPlanNeedW : 0) |
               (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) |
               (eu >= 1 ? kPlanSpec | (eu << kPlanEuShift) : 0) |
@@ -450,9 +449,9 @@ __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales,
 template <int LOGN>
 __global__ void __launch_bounds__(WctGeom<LOGN>::BLOCK) wct_spectra_plan(CwtArgs a, cpx* __restrict__ spec,
                                                                          int K, int dec, int wide,
-                                                                         int direct, int* __restrict__ plan) {
+                                                                         int* __restrict__ plan) {
   if (blockIdx.x + 1 == gridDim.x)
-    wct_plan_body<LOGN>(a.scales, a.S, a.dt, a.f0, K, a.prune, dec, wide, direct, a.batch, plan,
+    wct_plan_body<LOGN>(a.scales, a.S, a.dt, a.f0, K, a.prune, dec, wide, a.batch, plan,
                         plan + a.S + 1);
   else
     spectra_body<LOGN>(a, spec, blockIdx.x);
@@ -611,15 +610,15 @@ __device__ __forceinline__ void wct_dec_rows(const CwtArgs& a, const WctRowCtx& 
       band_load<LOGN, E>(pre, c.TA + rowbase, t);
     else if (more)
       band_load<LOGN, E>(pre, dy_row(r + G::ROWS), t);
-    if (valid) xwt_outputs<LOGN, BUF>(a, v, rowbase, t);
+    if (valid) xwt_outputs<LOGN, BUF, true>(a, v, rowbase, t);
     if (tpath) {
       const bool wr = valid && (c.plan[c.j0 + (valid ? jl : r0)] & kPlanNeedT);
       band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // (T1, T2)
       band_load<LOGN, E>(pre, c.TB + rowbase, t);
-      if (wr) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      if (wr) put_row<LOGN, BUF, true>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // T12
       if (more) band_load<LOGN, E>(pre, dy_row(r + G::ROWS), t);
-      if (wr) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return v[m]; });
+      if (wr) put_row<LOGN, BUF, true>(c.TB + rowbase, t, n0, [&](int m) { return v[m]; });
     }
   }
 }
@@ -629,131 +628,6 @@ __device__ __forceinline__ void wct_dec_rows(const CwtArgs& a, const WctRowCtx& 
 //   Q = 0: W1, W2 -> z1 = |W1|^2 + i |W2|^2, W12 -> full smoothing transforms of both.
 //   Q >= 1: pruned inverse transforms, and once each forward transform is done only the one
 //   band bin per thread is kept (2 VGPRs), so W12's outputs and transforms run with z1 dead.
-// Time smoothing by direct convolution (plan bit kPlanDirect) of one field held in the FFT
-// layout (v[m] at position t + m NT): out[p] = sum_{|d| <= R} g[|d|] v[(p - d) mod N], g the
-// sampled Gaussian of the row times 1/s; lane d of the wave holds g[d] in gl, the taps are read
-// into SGPRs and broadcast by v_pk_fma_f32's op_sel.  The transforms' kernel ifft(F) / N is
-// that Gaussian periodised, up to the spectrum's cut at N/2 (below exp(-sigma^2 pi^2 / 2) = 3e-9
-// for sigma >= 2).  LDS copy of the row: position p at j = p + H (halos: positions [N - H, N) at
-// j < H, [0, H) at j >= N + H, so no window wraps), padded index j + j/32.  Thread u convolves
-// positions 16u .. 16u + 15 from the 16 + 2R positions around them: with u = 2u' + h the padded
-// index of 16u + q is A_h + (a compile-time offset of q), so every window read is one ds_read_b64
-// off one of two base registers, and for a fixed q the lanes' reads cover the 64 banks once per
-// half wave.  The result returns through LDS to the FFT layout, for put_row.
-template <int LOGN>
-struct DirectGeom {
-  static constexpr int EXTRA =
-      LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn ? 3 * kDirectHalo : 0;  // the halo copy's LDS
-};
-__host__ __device__ constexpr int floor32(int q) { return q >= 0 ? q / 32 : -((31 - q) / 32); }
-template <int LOGN, int R>
-__device__ __forceinline__ void direct_smooth(cpx (&v)[16], cpx* my, int t, int u, float gl) {
-  using P = FftPlan<LOGN>;
-  constexpr int H = kDirectHalo;
-  static_assert(R + 1 <= H && H <= P::NT && P::NT >= kWave, "halo covers the window, m = 0 / 15 slots");
-  __syncthreads();  // the row buffer's previous readers are done
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    const int j = t + m * P::NT + H;
-    my[j + (j >> 5)] = v[m];
-  }
-  if (t >= P::NT - H) {  // positions N - H .. N - 1 (m = 15) before the row
-    const int j = t + 15 * P::NT - P::N + H;
-    my[j + (j >> 5)] = v[15];
-  }
-  if (t < H) {  // positions 0 .. H - 1 (m = 0) after it
-    const int j = t + P::N + H;
-    my[j + (j >> 5)] = v[0];
-  }
-  __syncthreads();
-  float g[R + 1];
-#pragma unroll
-  for (int d = 0; d <= R; ++d)
-    g[d] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gl), d));
-  // padded index of position 16u + q: (q mod 32 < 16 ? A0 : A1) + q + R + 1 + floor(q / 32)
-  const int a0 = 16 * u + (u >> 1) + H + 1 - R - 1;
-  const cpx* b0 = my + a0;
-  const cpx* b1 = my + a0 + (u & 1);
-  cpx acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = mkc(0.f, 0.f);
-#pragma unroll
-  for (int q = -R; q < 16 + R; ++q) {
-    const cpx x = ((q - 32 * floor32(q)) < 16 ? b0 : b1)[q + R + 1 + floor32(q)];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int d = q < i ? i - q : q - i;
-      if (d <= R) acc[i] = cfma(x, mkc(g[d], g[d]), acc[i]);
-    }
-  }
-  __syncthreads();  // every window read is done before the row is overwritten
-  cpx* w0 = my + a0 + R + 1;  // position 16u + i at w0[i]
-#pragma unroll
-  for (int i = 0; i < 16; ++i) w0[i] = acc[i];
-  __syncthreads();
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    const int j = t + m * P::NT + H;
-    v[m] = my[j + (j >> 5)];
-  }
-}
-
-template <int LOGN, bool BUF, int R>
-__device__ __forceinline__ void direct_fields(const CwtArgs& a, const WctRowCtx& c, cpx (&w1)[16], cpx (&v)[16],
-                                              cpx* my, int t, int u, float gl, bool valid, long long rowbase) {
-  direct_smooth<LOGN, R>(w1, my, t, u, gl);
-  if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, a.n0, [&](int m) { return w1[m]; });  // smoothed W12/s
-  direct_smooth<LOGN, R>(v, my, t, u, gl);
-  if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, a.n0, [&](int m) { return v[m]; });
-}
-
-// Direct rows (plan bit kPlanDirect; phase A kind 3): W1, W2 by inverse transforms as the other
-// full-band rows, the XWT outputs, then both fields smoothed by direct convolution
-// (direct_smooth) into the time-domain workspace -- two transforms per row instead of six.
-template <int LOGN, bool FULL, bool TWL, int NZ>
-__device__ __forceinline__ void wct_rows_direct(const CwtArgs& a, const WctRowCtx& c, int r0, int r1, cpx* my,
-                                                const cpx* tw, int g, int t, int& par, const float4* twl) {
-  using P = FftPlan<LOGN>;
-  using G = WctGeom<LOGN>;
-  constexpr bool BUF = P::NT >= kWave;
-  const float f0 = static_cast<float>(a.f0);
-  const int n0 = a.n0;
-  const int u = static_cast<int>(threadIdx.x) - g * P::NT;
-  const float ln = static_cast<float>(__lane_id());
-  for (int r = r0; r < r1; r += G::ROWS) {
-    const int jl = r + g;
-    const bool valid = jl < r1;
-    const cpx prm = c.prm_tab[valid ? jl : r0];
-    const long long rowbase = (c.b * a.S + c.j0 + (valid ? jl : r0)) * static_cast<long long>(n0);
-    cpx w1[16], v[16];
-    wct_inverse_row<LOGN, 0, TWL, NZ>(v, c.spec1, prm, f0, my, tw, t, par, twl);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) w1[m] = v[m];
-    wct_inverse_row<LOGN, 0, TWL, NZ>(v, c.spec2, prm, f0, my, tw, t, par, twl);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {  // W12, z1 = |W1|^2 + i |W2|^2, zero past n0
-      const int pos = t + m * P::NT;
-      const cpx w12 = cmul2_conj(w1[m], v[m]);
-      const cpx z1 = mkc(cabs2(w1[m]), cabs2(v[m]));
-      const bool in = FULL || pos < n0;
-      w1[m] = in ? w12 : mkc(0.f, 0.f);
-      v[m] = in ? z1 : mkc(0.f, 0.f);
-    }
-    if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
-    const double s = a.scales[c.j0 + (valid ? jl : r0)];
-    const double sg = s / a.dt;  // the Gaussian's sigma in samples
-    const float ce = static_cast<float>(-0.5 * 1.44269504088896340736 / (sg * sg));
-    const float amp = static_cast<float>(1.0 / (2.50662827463100050242 * sg * s));
-    const float gl = amp * __builtin_amdgcn_exp2f(ce * ln * ln);
-    // tap class of the iteration's widest row (rows ascend in scale; workgroup-uniform)
-    const double sg_max = a.scales[c.j0 + min(r + G::ROWS, r1) - 1] / a.dt;
-    if (sg_max * kBandT <= kDirectR0 + 1)
-      direct_fields<LOGN, BUF, kDirectR0>(a, c, w1, v, my, t, u, gl, valid, rowbase);
-    else
-      direct_fields<LOGN, BUF, kDirectR1>(a, c, w1, v, my, t, u, gl, valid, rowbase);
-  }
-}
-
 template <int LOGN, bool FULL, int Q, bool TWL, int NZ = 16>
 __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, int r0, int r1, cpx* my,
                                          const cpx* tw, int g, int t, int& par, const float4* twl) {
@@ -791,7 +665,7 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       fft_row<LOGN, 1, 1, TWL, 2>(v, my, 0, tw, t, par, twl);
 #pragma unroll
       for (int m = 0; m < 16; ++m) w1[m] = cmul2_conj(w1[m], v[m]);
-      if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
+      if (valid) xwt_outputs<LOGN, BUF, FULL>(a, w1, rowbase, t);
       cpx zy = mkc(0.f, 0.f), wy = mkc(0.f, 0.f);
       const int k = t - P::NT / 2;  // band-workspace index t <-> bin k
       const bool holder = k >= -K0 && k < K0;
@@ -828,9 +702,9 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       if (pl & kPlanNeedT) {
         const int slot = holder ? k + K0 : -1;
         smooth_from_band<LOGN, 2, TWL>(w1, wy, slot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+        if (valid) put_row<LOGN, BUF, FULL>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
         smooth_from_band<LOGN, 2, TWL>(v, zy, slot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+        if (valid) put_row<LOGN, BUF, FULL>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       }
       continue;
     }
@@ -863,21 +737,21 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       if (pl_any & kPlanNeedT) {
         fft_row<LOGN, 1, 1, TWL>(v, my, 0, tw, t, par, twl);
         // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
-        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF, FULL>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       }
       // the XWT-shaped outputs once z1 is dead (only W12 live: no spills around atan2)
-      if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
+      if (valid) xwt_outputs<LOGN, BUF, FULL>(a, w1, rowbase, t);
       fft_row<LOGN, -1, 1, TWL>(w1, my, 0, tw, t, par, twl);
       smooth_filter<LOGN>(w1, smt.x, smt.y, t);
       if (wb) wb_put_full<LOGN>(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 1), mw, w1, t);
       if (pl_any & kPlanNeedT) {
         fft_row<LOGN, 1, 1, TWL>(w1, my, 0, tw, t, par, twl);
-        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });
+        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF, FULL>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });
       }
     } else {
       int zslot, wslot;
       const cpx zy = smooth_band_bin<LOGN, Q>(v, smt, t, zslot);
-      if (valid) xwt_outputs<LOGN, BUF>(a, w1, rowbase, t);
+      if (valid) xwt_outputs<LOGN, BUF, FULL>(a, w1, rowbase, t);
       fft_row<LOGN, -1, 1, TWL>(w1, my, 0, tw, t, par, twl);
       const cpx wy = smooth_band_bin<LOGN, Q>(w1, smt, t, wslot);
       const int pl = c.plan[c.j0 + (valid ? jl : r0)];
@@ -899,9 +773,9 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       }
       if (pl_any & kPlanNeedT) {
         smooth_from_band<LOGN, Q, TWL>(w1, wy, wslot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+        if (valid) put_row<LOGN, BUF, FULL>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
         smooth_from_band<LOGN, Q, TWL>(v, zy, zslot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+        if (valid) put_row<LOGN, BUF, FULL>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       }
     }
   }
@@ -911,23 +785,18 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
 // other non-decimated rows (regimes 1, 2), 2 the decimated rows (plan e > 0).  Separate
 // launches over the same chunk grid, so that each row kind gets its own kernel's register
 // budget (one kernel for kinds 0 and 1 spilled 128 bytes per lane on LOGN 13, kind 0 alone 48).
-// 3 the direct rows (plan bit kPlanDirect, option wct_direct, off by default: full-band time-path
-// rows smoothed by direct convolution; their kernel takes the 256-VGPR budget of one 512-thread
-// workgroup per CU -- in the 128-VGPR kind-0 kernel the unrolled convolution spilled -- and is
-// slower than the transforms it replaces at every measured size).
 template <int LOGN> __device__ __forceinline__ int phase_a_kind(int pl) {
-  return plan_dec(pl) > 0 ? 2 : (pl & kPlanDirect) ? 3 : ((pl & kPlanQ) == 0 ? 0 : 1);
+  return plan_dec(pl) > 0 ? 2 : ((pl & kPlanQ) == 0 ? 0 : 1);
 }
 template <int LOGN, bool FULL, int KIND>
-__global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (KIND == 3 ? 2 : WctGeom<LOGN>::MINW))
+__global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     wct_phase_a(CwtArgs a, const cpx* __restrict__ spec, cpx* __restrict__ TA, cpx* __restrict__ TB,
                 cpx* __restrict__ SB, const cpx* __restrict__ DY, cpx* __restrict__ WB,
                 const int* __restrict__ plan) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
   constexpr int BAND_F4 = LOGN >= 12 ? (P::N >> 8) : 1;  // 2 * (N >> 8) complex
-  // row buffers: the FFT exchange (PADN), or for direct rows also the halo copy (direct_smooth)
-  constexpr int CSTR = P::PADN + (KIND == 3 ? DirectGeom<LOGN>::EXTRA : 0);
+  constexpr int CSTR = P::PADN;  // row buffers: the FFT exchange
   __shared__ float4 lds4[(G::ROWS * CSTR) / 2 + G::MAXCHUNK + G::TWL_F4 + G::MAXCHUNK / 4 + BAND_F4];
   cpx* lds = reinterpret_cast<cpx*>(lds4);
   cpx* prm_tab = lds + G::ROWS * CSTR;         // (alpha, log2 c) of the Morlet filter
@@ -952,8 +821,8 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (KIND == 3 ? 2 : WctGe
 
   for (int i = tid; i < j1 - j0; i += G::BLOCK) {
     const int pl = plan[j0 + i];
-    // run key: the regime, 4 + e for decimated rows, 16 for direct rows
-    q_tab[i] = plan_dec(pl) > 0 ? 4 + plan_dec(pl) : (pl & kPlanDirect) ? 16 : (pl & kPlanQ);
+    // run key: the regime, 4 + e for decimated rows
+    q_tab[i] = plan_dec(pl) > 0 ? 4 + plan_dec(pl) : (pl & kPlanQ);
     if (KIND == 2) continue;  // decimated rows need no filter tables
     const double s = a.scales[j0 + i];
     prm_tab[i] = morlet_params(s, a.dt, P::N);
@@ -993,14 +862,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (KIND == 3 ? 2 : WctGe
     const int q = q_tab[r0];
     int r1 = r0 + 1;
     while (r1 < nrow && q_tab[r1] == q) ++r1;
-    if (q == 16) {  // direct rows
-      if constexpr (KIND == 3 && LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) {
-        if (a.prune && a.f0 >= kBandF0 && P::NT >= 16)  // negative frequencies dropped: half the bins
-          wct_rows_direct<LOGN, FULL, TWL, 8>(a, c, r0, r1, my, tw, g, t, par, twl);
-        else
-          wct_rows_direct<LOGN, FULL, TWL, 16>(a, c, r0, r1, my, tw, g, t, par, twl);
-      }
-    } else if (q >= 4) {  // decimated rows (full rows only)
+    if (q >= 4) {  // decimated rows (full rows only)    } else if (q >= 4) {  // decimated rows (full rows only)
       if constexpr (KIND == 2 && FULL && LOGN >= kDecMinLogn) {
         switch (q - 4) {
 #define WTMI_DR(EE)                                                                     \
@@ -1317,7 +1179,7 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
 //   S1 + i S2 = IFFT(sum_q w_q Z_q),   S12 = IFFT(sum_q w_q W_q),   WCT = |S12|^2 / (S1 S2).
 // These rows skip the time-domain workspace (16 B per coefficient written by phase A and
 // read back by phase B) and phase A's smoothing transforms move here.
-template <int LOGN, int Q, bool BUF, bool TWL>
+template <int LOGN, int Q, bool BUF, bool TWL, bool FULL>
 __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __restrict__ SB, int K,
                                               long long b, int j0, int r0, int r1, cpx* my, const cpx* tw,
                                               int g, int t, int& par, const float4* twl,
@@ -1372,7 +1234,7 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
     smooth_from_band<LOGN, Q, TWL, false>(v, yw, slot, my, tw, t, par, twl);
     if (valid) {
       const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
-      put_row<LOGN, BUF>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
+      put_row<LOGN, BUF, FULL>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
     }
   }
 }
@@ -1454,7 +1316,7 @@ __global__ void __launch_bounds__(256) wct_wide_boxcar(cpx* __restrict__ WB, lon
 // narrowed to NZ = 16 >> EU inputs) -- S1 + i S2 and S12 at every sample -- and WCT is written.
 // Replaces, for these rows, phase A's two inverse smoothing transforms per row, the 16-byte
 // time-domain workspace write and phase B's read of it.
-template <int LOGN, int EU, bool BUF, bool TWL>
+template <int LOGN, int EU, bool BUF, bool TWL, bool FULL>
 __device__ __forceinline__ void wct_wide_rows(const CwtArgs& a, const cpx* __restrict__ WB, long long b,
                                               int j0, int r0, int r1, cpx* my, const cpx* tw, int g, int t,
                                               int& par, const float4* twl, float* __restrict__ coh) {
@@ -1480,7 +1342,7 @@ __device__ __forceinline__ void wct_wide_rows(const CwtArgs& a, const cpx* __res
     band_ifft<LOGN, EU, TWL>(v, pre, my, tw, t, par, twl);
     if (valid) {
       const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
-      put_row<LOGN, BUF>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
+      put_row<LOGN, BUF, FULL>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
     }
   }
 }
@@ -1533,15 +1395,15 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     int r1 = r0 + 1;
     while (r1 < nrow && key(r1) == q) ++r1;
     if constexpr (!WIDE && P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
-      if (q == 1) wct_spec_rows<LOGN, 1, BUF, TWL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      if (q == 1) wct_spec_rows<LOGN, 1, BUF, TWL, FULL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
       if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
-        if (q == 2) wct_spec_rows<LOGN, 2, BUF, TWL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+        if (q == 2) wct_spec_rows<LOGN, 2, BUF, TWL, FULL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
       }
     }
     if constexpr (WIDE && LOGN >= kWideMinLogn) {
-      if (q == 5) wct_wide_rows<LOGN, 1, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
-      if (q == 6) wct_wide_rows<LOGN, 2, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
-      if (q == 7) wct_wide_rows<LOGN, 3, BUF, TWL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      if (q == 5) wct_wide_rows<LOGN, 1, BUF, TWL, FULL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      if (q == 6) wct_wide_rows<LOGN, 2, BUF, TWL, FULL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
+      if (q == 7) wct_wide_rows<LOGN, 3, BUF, TWL, FULL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
     }
     r0 = r1;
   }
@@ -1563,34 +1425,95 @@ static int wct_dec_rows_per_wg(long long batch) {
   return o > 0 ? o : (batch <= 256 ? 8 : 4);
 }
 
-// Side stream of the calling thread on the current device (created once; thread_local, so
-// concurrent callers never share one): the full-band rows' kernel runs there beside the
-// decimated rows' chain (fork after the plan, join before the spectral boxcar).  A small batch
-// (one GPU's shard of a strong-scaling run) leaves CUs idle in each kernel; two independent
-// kernels in flight fill them.
+// Side streams for the full-band rows' kernel beside the decimated rows' chain (fork after the
+// plan, join before the caller's stream proceeds).  A small batch (one GPU's shard of a
+// strong-scaling run) leaves CUs idle in each kernel; two independent kernels in flight fill
+// them.  One stream + four events per concurrent caller, from a per-device pool: a call
+// takes one (or creates one when all are in use) and hands it back after its last enqueue, so
+// the pool holds as many as calls ever overlapped, however many host threads come and go (a
+// thread_local stream per thread leaked one per short-lived thread: a Streamlit rerun runs on a
+// fresh ScriptRunner thread).  Reuse is safe: hipStreamWaitEvent waits on the event's record
+// at the time of the call, and the next owner's work follows on the same side stream.
 struct SideStream {
   hipStream_t s = nullptr;
   // fork: spectra + plan done (main); k0: full-band rows done (side); dec: decimated spectra
   // done (main); join: the side stream's last kernel done
   hipEvent_t fork = nullptr, k0 = nullptr, dec = nullptr, join = nullptr;
 };
-static SideStream* side_stream() {
-  constexpr int kMaxDev = 64;
-  thread_local SideStream tl[kMaxDev];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
-  SideStream& ss = tl[dev];
-  if (!ss.s) {
-    if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return ss.s = nullptr, nullptr;
-    for (hipEvent_t* e : {&ss.fork, &ss.k0, &ss.dec, &ss.join})
-      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
-  }
-  return &ss;
+namespace {
+constexpr int kMaxDev = 64;
+struct SidePool {
+  std::mutex mu;
+  std::vector<SideStream*> idle[kMaxDev];
+  std::atomic<long long> created{0};
+};
+// Never destroyed: the streams live as long as the process (the HIP runtime tears itself down
+// at exit; destroying streams from a static destructor after that is undefined).
+SidePool& side_pool() {
+  static SidePool* p = new SidePool;
+  return *p;
 }
+SideStream* side_acquire(int& dev) {
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  SidePool& pool = side_pool();
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    if (!pool.idle[dev].empty()) {
+      SideStream* ss = pool.idle[dev].back();
+      pool.idle[dev].pop_back();
+      return ss;
+    }
+  }
+  SideStream* ss = new SideStream;
+  bool ok = hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t* e : {&ss->fork, &ss->k0, &ss->dec, &ss->join})
+    ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    for (hipEvent_t e : {ss->fork, ss->k0, ss->dec, ss->join})
+      if (e) (void)hipEventDestroy(e);
+    if (ss->s) (void)hipStreamDestroy(ss->s);
+    delete ss;
+    (void)hipGetLastError();
+    return nullptr;  // the call runs single-stream
+  }
+  pool.created.fetch_add(1);
+  return ss;
+}
+void side_release(SideStream* ss, int dev) {
+  SidePool& pool = side_pool();
+  std::lock_guard<std::mutex> lk(pool.mu);
+  pool.idle[dev].push_back(ss);
+}
+}  // namespace
+
+// Owns a call's side stream: on every return after the fork -- success or a failed launch /
+// event call -- the side stream records `join` and the caller's stream waits on it before the
+// stream goes back to the pool, so no side-stream kernel can still be writing the workspace
+// or the outputs once the caller's stream is past the call.
+struct SideJoin {
+  SideStream* side = nullptr;
+  hipStream_t st = nullptr;
+  int dev = 0;
+  bool forked = false;
+  SideJoin(bool want, hipStream_t caller) : st(caller) {
+    if (want) side = side_acquire(dev);
+  }
+  ~SideJoin() {
+    if (!side) return;
+    if (forked) {
+      (void)hipEventRecord(side->join, side->s);
+      (void)hipStreamWaitEvent(st, side->join, 0);
+    }
+    side_release(side, dev);
+  }
+  SideJoin(const SideJoin&) = delete;
+  SideJoin& operator=(const SideJoin&) = delete;
+};
 
 template <int LOGN>
 static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY, cpx* WB, int* plan,
-                          int K, float* coh, hipStream_t st, SideStream* side) {
+                          int K, float* coh, hipStream_t st, SideJoin& sj) {
+  SideStream* side = sj.side;
   using G = WctGeom<LOGN>;
   const long long sgrid = (2 * a.batch + G::ROWS - 1) / G::ROWS;  // spectra workgroups
   if (sgrid + 1 > 0x7fffffffll) return kErrUnsupported;
@@ -1616,11 +1539,8 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   if (grid > 0x7fffffffll || a.batch * a.S > 0x7fffffffll - 64) return kErrUnsupported;
   // decimated rows: full rows, pruning level 2, Morlet negative frequencies negligible
   const int dec = (a.prune >= 2 && a.n0 == (1 << LOGN) && LOGN >= kDecMinLogn && a.f0 >= kBandF0) ? 1 : 0;
-  // direct rows (kPlanDirect) and their kernel (phase A kind 3)
-  const int direct =
-      (options().wct_direct && a.prune && LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) ? 1 : 0;
   hipLaunchKernelGGL(wct_spectra_plan<LOGN>, dim3(static_cast<unsigned>(sgrid + 1)), dim3(G::BLOCK), 0, st, a,
-                     spec, K, dec, options().wct_wide, direct, plan);
+                     spec, K, dec, options().wct_wide, plan);
   int rc = launch_status();
   if (rc != kOk) return rc;
   const dim3 gd(static_cast<unsigned>(grid));
@@ -1628,13 +1548,6 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
     hipLaunchKernelGGL((wct_phase_a<LOGN, false, 0>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
                        plan);
     if ((rc = launch_status()) != kOk) return rc;
-    if constexpr (LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) {
-      if (direct) {
-        hipLaunchKernelGGL((wct_phase_a<LOGN, false, 3>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY,
-                           WB, plan);
-        if ((rc = launch_status()) != kOk) return rc;
-      }
-    }
     if (a.prune) {  // band rows exist only with pruning
       hipLaunchKernelGGL((wct_phase_a<LOGN, false, 1>), gd, dim3(G::BLOCK), 0, st, a, spec, TA, TB, SB, DY, WB,
                          plan);
@@ -1646,20 +1559,14 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   // caller joins it) -- then the decimated rows' spectra and their kernel.
   hipStream_t sa = st;
   if (side) {
-    if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
-      return launch_status();
+    if (hipEventRecord(side->fork, st) != hipSuccess) return launch_status();
+    sj.forked = true;
+    if (hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess) return launch_status();
     sa = side->s;
   }
   hipLaunchKernelGGL((wct_phase_a<LOGN, true, 0>), gd, dim3(G::BLOCK), 0, sa, a, spec, TA, TB, SB, DY, WB,
                      plan);
   if ((rc = launch_status()) != kOk) return rc;
-  if constexpr (LOGN >= kDirectMinLogn && LOGN <= kDirectMaxLogn) {
-    if (direct) {
-      hipLaunchKernelGGL((wct_phase_a<LOGN, true, 3>), gd, dim3(G::BLOCK), 0, sa, a, spec, TA, TB, SB, DY, WB,
-                         plan);
-      if ((rc = launch_status()) != kOk) return rc;
-    }
-  }
   if (side && hipEventRecord(side->k0, side->s) != hipSuccess) return launch_status();
   // band rows that are not decimated: none when the decimation is on (a row of regime >= 1 has
   // its CWT band within N/16, hence a decimation M <= N/8), so that launch is skipped then
@@ -1995,12 +1902,12 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
   int rc;
   // side stream for the full-band rows beside the decimated chain (full rows with decimation:
   // LOGN >= kDecMinLogn, n0 = N, pruning 2), option wct_side_stream
-  SideStream* side = nullptr;
-  if (options().wct_side_stream && logn >= kDecMinLogn && n0 == (1ll << logn) && options().wct_prune >= 2 &&
-      f0 >= kBandF0)
-    side = side_stream();
+  SideJoin sj(options().wct_side_stream && logn >= kDecMinLogn && n0 == (1ll << logn) &&
+                  options().wct_prune >= 2 && f0 >= kBandF0,
+              st);
+  SideStream* side = sj.side;
   switch (logn) {
-#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, WB, plan, boxcar, out_coh, st, side); break;
+#define WTMI_A(L) case L: rc = launch_phase_a<L>(a, spec, TA, TB, SB, DY, WB, plan, boxcar, out_coh, st, sj); break;
     WTMI_A(4) WTMI_A(5) WTMI_A(6) WTMI_A(7) WTMI_A(8) WTMI_A(9) WTMI_A(10) WTMI_A(11)
     WTMI_A(12) WTMI_A(13) WTMI_A(14)
 #undef WTMI_A
@@ -2045,13 +1952,8 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
     if ((rc = launch_status()) != kOk) return rc;
   }
   if ((rc = phase_c(sc)) != kOk) return rc;
-  if (side) {
-    if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->k0, 0) != hipSuccess)
-      return launch_status();
-    if ((rc = wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st)) != kOk) return rc;
-    if (hipStreamWaitEvent(st, side->join, 0) != hipSuccess) return launch_status();
-    return kOk;
-  }
+  // phase B on the caller's stream once the full-band rows are done; sj joins the side stream
+  if (side && hipStreamWaitEvent(st, side->k0, 0) != hipSuccess) return launch_status();
   return wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st);
 }
 
@@ -2071,3 +1973,7 @@ extern "C" int wtmi_wct_morlet_norm(const float* x1, const float* x2, long long 
   return wct_morlet_impl(x1, x2, ld, batch, n0, nullptr, nullptr, 1, scales, n_scales, dt, f0, boxcar, workspace,
                          out_coh, out_power, out_phase, out_u, out_v, stream);
 }
+
+// Side streams the WCT has created in this process (all devices): the pool's size, i.e. the
+// most full-row WCT calls that ever ran at once, not the number of threads that made one.
+extern "C" long long wtmi_wct_side_streams(void) { return wtmi::side_pool().created.load(); }

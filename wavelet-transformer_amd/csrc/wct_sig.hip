@@ -36,16 +36,22 @@ __device__ __forceinline__ double u01(unsigned a, unsigned b) {  // (0, 1), 53 b
   return (static_cast<double>(v & ((1ull << 53) - 1)) + 0.5) * 0x1.0p-53;
 }
 
-// K10: AR(1) red noise, pycwt helpers.rednoise(N, g, a=1):
-//   y = lfilter([1, 0], [1, -g], randn(N + tau))[tau:], tau = ceil(-2 / ln|g|).
-// Normal i of series sid comes from Philox block (i / 2, sid) by Box-Muller (fp64).  One
-// workgroup per series; the recurrence y_i = g y_{i-1} + e_i is split into 256 chunks of L
-// consecutive samples: pass 1 runs each chunk from a zero state (its end value a_c), one
+// K10: pycwt helpers.rednoise(N, g, a=1) (pycwt 0.4.0b0):
+//   yr = lfilter([1, 0], [1, -g], np.random.randn(N + tau, 1) * a)[tau:], tau = ceil(-2 / ln|g|).
+// lfilter runs along its default axis -1, which has length 1 for that (N + tau, 1) array, so
+// the filter is the identity and pycwt's noise is WHITE (N normals; g only sets tau).  That
+// literal reading is the default (filtered = 0: DESIGN 4, "Monte-Carlo noise").  filtered = 1
+// runs the AR(1) recurrence y_i = g y_{i-1} + e_i that Grinsted's MATLAB rednoise.m (whose
+// filter works along the first non-singleton dimension) intends.
+// Normal i of series sid comes from Philox block (i / 2, sid) by Box-Muller (fp64); both modes
+// draw the same normals.  One workgroup per series; the recurrence is split into 256 chunks of
+// L consecutive samples: pass 1 runs each chunk from a zero state (its end value a_c), one
 // thread chains the chunks' carries (carry_c = g^L carry_{c-1} + a_{c-1}), pass 2 reruns each
 // chunk from its carry -- regenerating the same normals -- and writes y.  The sequential
 // recurrence of one thread per series took milliseconds per launch (N + tau ~ 8000 steps of
 // Philox + fp64 log / sincospi each); this is the same linear recurrence in a different
-// summation order (fp64, rounded to fp32 on store).
+// summation order (fp64, rounded to fp32 on store).  With g = 0 (the white mode) every step is
+// fma(0, y, e) = e exactly.
 __device__ __forceinline__ void rn_normals(unsigned long long sid, uint2 key, int i0, double (&e)[2]) {
   const uint4 w = Philox::gen(make_uint4(static_cast<unsigned>(i0 >> 1), static_cast<unsigned>(sid),
                                          static_cast<unsigned>(sid >> 32), 0x5eed5u), key);
@@ -217,8 +223,9 @@ __global__ void __launch_bounds__(kQThreads) coherence_quantile_kernel(const uns
 
 using namespace wtmi;
 
-extern "C" int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g,
+extern "C" int wtmi_rednoise(float* out, long long ld, long long count, long long n, double g, int filtered,
                              unsigned long long seed, unsigned long long first_series, void* stream) {
+  if (filtered != 0 && filtered != 1) return kErrArg;
   if (count < 0 || n < 0 || ld < n || !(g > -1.0 && g < 1.0)) return kErrArg;
   if (n > (1ll << 30)) return kErrUnsupported;
   if (count == 0 || n == 0) return kOk;  // empty batch: no-op (NULL arrays allowed)
@@ -231,7 +238,7 @@ extern "C" int wtmi_rednoise(float* out, long long ld, long long count, long lon
   }
   if (count > 0x7fffffffll) return kErrUnsupported;
   hipLaunchKernelGGL(rednoise_kernel, dim3(static_cast<unsigned>(count)), dim3(kRnThreads), 0,
-                     static_cast<hipStream_t>(stream), out, ld, count, static_cast<int>(n), g, tau, seed,
+                     static_cast<hipStream_t>(stream), out, ld, count, static_cast<int>(n), filtered ? g : 0.0, tau, seed,
                      first_series);
   return launch_status();
 }

@@ -92,5 +92,12 @@ def create_cwt_results_dict(cwt_data_dict: dict[str, DataForCWT], measures_list:
 
 def create_xwt_results_dict(xwt_data_dict: dict[str, DataForXWT], xwt_list: list[tuple[str, str]],
                             **kwargs) -> ResultsFromXWT:
-    """run_xwt per pair (:126-135), batched: one XWT launch (+ one phase launch) per group."""
-    return dict(zip(xwt_list, xwt.run_xwt_batch([xwt_data_dict[c] for c in xwt_list], **kwargs)))
+    """run_xwt per pair (:126-135), batched: one XWT launch (+ one phase launch) per group.
+    Fails as run_xwt(data, **kwargs) does in the reference: unknown keywords raise TypeError,
+    normalize=False NameError, a non-Morlet mother AttributeError."""
+    unknown = sorted(set(kwargs) - {"normalize"})
+    if unknown:
+        raise TypeError(f"run_xwt() got unexpected keyword arguments {unknown}")
+    if not kwargs.get("normalize", True):
+        raise NameError("name 'signal_size' is not defined")
+    return dict(zip(xwt_list, xwt.run_xwt_batch([xwt_data_dict[c] for c in xwt_list])))

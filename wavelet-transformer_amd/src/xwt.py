@@ -4,12 +4,14 @@
 the significance ratio come from one pair-mode HIP kernel launch; the phase arrows
 from a second launch at the scales pycwt.wct would use -- the reference passes
 ``delta_j=`` to ``wct`` which swallows it, so the phase runs at dj = 1/12
-(quirk B.5).  ``normalize=False`` raises NameError in the reference (B.7); here it
-returns the raw complex cross spectrum (documented deviation).  Non-Morlet mothers
-(``MOTHER_DICT["paul"]``, ``["DOG"]``, ``["mexicanhat"]``): the power and significance
-are pycwt.xwt's for that mother; the reference then fails inside pycwt.wct (only Morlet
-has ``smooth``), whereas here the phase is the angle of W1 W2* -- what pycwt.wct returns
-as aWCT, which needs no smoothing (documented deviation).
+(quirk B.5).  ``run_xwt`` fails where the reference fails: ``normalize=False`` raises
+NameError (B.7) and non-Morlet mothers (``MOTHER_DICT["paul"]``, ``["DOG"]``,
+``["mexicanhat"]``) raise AttributeError, as pycwt.wct does for a mother without
+``smooth``.  The engine extension ``run_xwt_batch`` offers both as explicit options:
+``normalize=False`` returns the raw complex cross spectrum, and
+``phase_without_smooth=True`` gives the non-Morlet mothers pycwt.xwt's power and
+significance with phase arrows from the angle of W1 W2* (what pycwt.wct returns as aWCT,
+which needs no smoothing).
 """
 
 from __future__ import annotations
@@ -23,7 +25,7 @@ import numpy.typing as npt
 import torch
 
 from wtmi import ops, transforms
-from wtmi.wavelets import DOG, MexicanHat, Morlet, Paul, as_mother, kernel_mother
+from wtmi.wavelets import DOG, MexicanHat, Morlet, Paul, as_morlet, as_mother, kernel_mother
 from src.utils import wavelet_helpers
 from src.utils.wavelet_helpers import coi_polygon
 
@@ -80,16 +82,35 @@ class ResultsFromXWT:
 
 def run_xwt(cross_wavelet_transform: Type[DataForXWT], normalize: bool = True
             ) -> Type[ResultsFromXWT]:
-    """Cross-wavelet power, period, significance ratio, COI polygon and phase arrows."""
+    """Cross-wavelet power, period, significance ratio, COI polygon and phase arrows.
+
+    As the reference does: ``normalize=False`` raises NameError (its else branch reads
+    ``signal_size``, bound only under ``normalize``; quirk B.7), and a Paul / DOG /
+    MexicanHat mother raises AttributeError (pycwt.wct has no ``smooth`` for it).  The
+    engine's alternatives are explicit: ``run_xwt_batch(..., normalize=False)`` (raw cross
+    spectrum) and ``run_xwt_batch(..., phase_without_smooth=True)``."""
+    if not normalize:
+        raise NameError("name 'signal_size' is not defined")
     return run_xwt_batch([cross_wavelet_transform], normalize=normalize)[0]
 
 
-def run_xwt_batch(xwt_data_list: List[DataForXWT], normalize: bool = True
-                  ) -> List[ResultsFromXWT]:
+def run_xwt_batch(xwt_data_list: List[DataForXWT], normalize: bool = True,
+                  phase_without_smooth: bool = False) -> List[ResultsFromXWT]:
     """``run_xwt`` over many pairs (engine extension; the reference loops in
     src/utils/transform_helpers.py:126-135).  Pairs of one length and transform
     parameters share one normalisation, one pair-mode XWT launch (per-pair AR(1)
-    significance as a [B, S] multiplier) and one phase launch."""
+    significance as a [B, S] multiplier) and one phase launch.
+
+    The reference takes the phase arrows from pycwt.wct (src/xwt.py:122-134), which needs
+    ``wavelet.smooth`` -- Morlet's only -- so for Paul / DOG / MexicanHat it raises
+    AttributeError, and so does this function by default (before any launch; the reference
+    would raise after its xwt, which has no side effect).  ``phase_without_smooth=True`` is
+    the engine's explicit alternative: the arrows from angle(W1 W2*) at dj = 1/12, which is
+    what pycwt.wct returns as aWCT and needs no smoothing."""
+    if not phase_without_smooth:
+        for d in xwt_data_list:
+            if kernel_mother(d.mother_wavelet)[0] != 0:
+                as_morlet(d.mother_wavelet)  # raises NoSmoothError (an AttributeError), as pycwt.wct
     out: List[ResultsFromXWT] = [None] * len(xwt_data_list)
     groups: dict = {}
     for i, d in enumerate(xwt_data_list):

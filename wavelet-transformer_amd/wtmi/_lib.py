@@ -38,7 +38,8 @@ PROTOTYPES = {
                                _P, _P, _P, _P, _P, _P, _P]),
     "wtmi_wct_morlet_norm": (_I32, [_P, _P, _I64, _I64, _I64, _P, _I32, _F64, _F64, _I32, _P, _P, _P, _P,
                                     _P, _P, _P]),
-    "wtmi_rednoise": (_I32, [_P, _I64, _I64, _I64, _F64, _U64, _U64, _P]),
+    "wtmi_wct_side_streams": (_I64, []),
+    "wtmi_rednoise": (_I32, [_P, _I64, _I64, _I64, _F64, _I32, _U64, _U64, _P]),
     "wtmi_coherence_histogram": (_I32, [_P, _I64, _I64, _I32, _P, _P, _I32, _I32, _P, _P]),
     "wtmi_coherence_quantile": (_I32, [_P, _I32, _I32, _F64, _P, _P]),
     "wtmi_modwt_workspace_bytes": (_I64, [_I64, _I64, _I32]),

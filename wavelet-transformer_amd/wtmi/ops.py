@@ -359,19 +359,32 @@ def wct_morlet(x1: torch.Tensor, x2: torch.Tensor, scales, dt: float, f0: float 
     return res
 
 
+NOISE_MODES = ("pycwt", "red")
+
+
 def rednoise(count: int, n: int, g: float, seed: int, *, first_series: int = 0,
-             device=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """[count, n] float32 AR(1) red noise (pycwt helpers.rednoise(n, g, 1) per row),
-    drawn on the GPU from Philox4x32-10 stream (seed, first_series + row)."""
+             device=None, out: Optional[torch.Tensor] = None, noise: str = "pycwt") -> torch.Tensor:
+    """[count, n] float32 Monte-Carlo noise, pycwt helpers.rednoise(n, g, 1) per row, drawn on
+    the GPU from Philox4x32-10 stream (seed, first_series + row).  noise="pycwt" (default) is
+    pycwt's literal behaviour: its lfilter runs along the length-1 axis of randn(n + tau, 1),
+    so the rows are white normals (g sets only the burn-in tau); noise="red" applies the AR(1)
+    filter the MATLAB original intends."""
+    if noise not in NOISE_MODES:
+        raise ValueError(f"noise must be one of {NOISE_MODES}, got {noise!r}")
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     if out is None:
         out = torch.empty((count, n), dtype=torch.float32, device=dev)
     _check_dev(out)
     with torch.cuda.device(out.device):
-        _lib.call("wtmi_rednoise", _ptr(out), out.stride(0), count, n, float(g),
+        _lib.call("wtmi_rednoise", _ptr(out), out.stride(0), count, n, float(g), int(noise == "red"),
                   C.c_ulonglong(int(seed) & ((1 << 64) - 1)), C.c_ulonglong(int(first_series)),
                   _stream(out.device))
     return out
+
+
+def wct_side_streams() -> int:
+    """Side streams the full-row WCT has created in this process (the pool's size)."""
+    return int(_lib.load().wtmi_wct_side_streams())
 
 
 def coherence_histogram(coh: torch.Tensor, t_lo: torch.Tensor, t_hi: torch.Tensor,

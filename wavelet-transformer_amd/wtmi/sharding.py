@@ -45,17 +45,23 @@ def _has_cpu_transport(group) -> bool:
 
 
 def host_group(group=None):
-    """A process group that can carry CPU tensors among the ranks of `group`: the group
-    itself under gloo, else a gloo side group made once (collective: every rank of `group`
-    reaches the first call together, as they do inside ``gather_to_rank0``)."""
+    """A process group that can carry CPU tensors among the ranks of the default group: the
+    group itself under gloo, else a gloo side group made once (collective: every rank of
+    the default group reaches the first call together, as they do inside
+    ``gather_to_rank0``).  Only the default group (None, or the WORLD group) is supported
+    under RCCL: torch requires EVERY process of the default group to call ``new_group``, even
+    for a subgroup, so building a side group lazily from a subgroup's ranks alone would hang.
+    The cache is keyed on the ranks, not on the group object's id (ids are reused after GC)."""
     if _has_cpu_transport(group):
         return group
-    key = id(group) if group is not None else None
+    if group is not None and group is not dist.group.WORLD:
+        raise ValueError("host_group: an RCCL subgroup is not supported (create a gloo group on "
+                         "every rank and pass that instead)")
+    key = tuple(range(dist.get_world_size()))
     with _HOST_LOCK:
         g = _HOST_GROUPS.get(key)
         if g is None:
-            ranks = None if group is None else dist.get_process_group_ranks(group)
-            g = dist.new_group(ranks=ranks, backend="gloo")
+            g = dist.new_group(ranks=list(key), backend="gloo")
             _HOST_GROUPS[key] = g
     return g
 

@@ -283,7 +283,7 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
             J = int(np.round(np.log2(n0 * dt / s0) / dj))
         a1, _, _ = ar1(y1)
         a2, _, _ = ar1(y2)
-        kw = {k: v for k, v in kwargs.items() if k in ("cache", "mc_count", "seed", "progress")}
+        kw = {k: v for k, v in kwargs.items() if k in ("cache", "mc_count", "seed", "progress", "noise")}
         sig = wct_significance(a1, a2, dt=dt, dj=dj, s0=s0, J=J,
                                significance_level=significance_level, wavelet=wavelet, **kw)
     else:
@@ -432,21 +432,36 @@ def sig_cache_store(key, sig95) -> None:
         pass
 
 
+# Monte-Carlo noise of wct_significance: "pycwt" (default) reproduces pycwt 0.4.0b0's
+# helpers.rednoise as published -- lfilter along the length-1 axis of randn(N + tau, 1), i.e.
+# white normals -- and "red" the AR(1) noise of Grinsted's MATLAB rednoise.m that it was ported
+# from ("Monte-Carlo noise"; parity unpinned: pycwt is absent from the image).
+SIG_NOISE = os.environ.get("WTMI_SIG_NOISE", "pycwt")
+
+
 def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="morlet",
                      mc_count=300, progress=True, cache=True, seed=None, nbins=1000,
-                     max_pairs_per_launch=512):
-    """pycwt ``wct_significance`` on the GPU: mc_count passes of two AR(1) red-noise
-    series (al1, al2), their coherence, and the per-scale counter of floor(R2 * nbins)
-    outside the COI, batched max_pairs_per_launch passes per launch.  ``cache`` keeps
-    results keyed on every argument, in process memory and on disk (``sig_cache_dir()``),
-    as pycwt's ``cache=True`` keeps them under the user cache dir (src/wct.py:117);
-    ``seed`` None draws a fresh one, as pycwt's unseeded draws do."""
+                     max_pairs_per_launch=512, noise=None):
+    """pycwt ``wct_significance`` on the GPU: mc_count passes of two noise series
+    (helpers.rednoise with al1, al2; ``noise`` "pycwt" or "red", default ``SIG_NOISE``),
+    their coherence, and the per-scale counter of floor(R2 * nbins) outside the COI, batched
+    max_pairs_per_launch passes per launch.  ``cache`` keeps results keyed on every argument,
+    in process memory and on disk (``sig_cache_dir()``), as pycwt's ``cache=True`` keeps them
+    under the user cache dir (src/wct.py:117); ``seed`` None draws a fresh one, as pycwt's
+    unseeded draws do.  Like pycwt's rednoise (whose g == 0 branch calls the nonexistent
+    ``np.randn``), a zero lag-1 coefficient raises AttributeError in the "pycwt" mode."""
     wavelet = as_morlet(wavelet)
     if wavelet.deltaj0 <= 0:
         raise ValueError("wct_significance needs a Morlet(6) wavelet (deltaj0 defined)")
+    noise = SIG_NOISE if noise is None else noise
+    if noise not in ops.NOISE_MODES:
+        raise ValueError(f"noise must be one of {ops.NOISE_MODES}, got {noise!r}")
+    if noise == "pycwt" and (float(al1) == 0.0 or float(al2) == 0.0):
+        raise AttributeError("module 'numpy' has no attribute 'randn' "
+                             "(pycwt helpers.rednoise with g == 0)")
     cache = cache and SIG_CACHE
-    key = ("wct_significance", 1, float(al1), float(al2), float(dt), float(dj), float(s0), int(J),
-           float(significance_level), wavelet.f0, int(mc_count), int(nbins), seed)
+    key = ("wct_significance", 2, noise, float(al1), float(al2), float(dt), float(dj), float(s0),
+           int(J), float(significance_level), wavelet.f0, int(mc_count), int(nbins), seed)
     if cache:
         hit = sig_cache_load(key)
         if hit is not None:
@@ -470,8 +485,8 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     ws = None
     for p0 in range(0, int(mc_count), max_pairs_per_launch):
         B = min(max_pairs_per_launch, int(mc_count) - p0)
-        n1 = ops.rednoise(B, N, al1, seed, first_series=p0, device=dev)
-        n2 = ops.rednoise(B, N, al2, seed, first_series=int(mc_count) + p0, device=dev)
+        n1 = ops.rednoise(B, N, al1, seed, first_series=p0, device=dev, noise=noise)
+        n2 = ops.rednoise(B, N, al2, seed, first_series=int(mc_count) + p0, device=dev, noise=noise)
         need = ops.wct_workspace_bytes(B, N, sj.size)
         if ws is None or ws.numel() < need:
             ws = torch.empty(need, dtype=torch.uint8, device=dev)
