@@ -9,11 +9,15 @@ inputs resident in HBM, one step = one transform of the whole batch.
 
 Multi-GPU: series (pairs) are independent, so the units shard across ranks with
 no collective on the data path; RCCL carries only the barrier and the max-over-ranks of the
-timed region.  Default ``--scaling weak``: rank r transforms its own block [r B, (r + 1) B) of a
-global batch of N B series (B = the config's batch: C2 1024 series, C3 8192, C4 512 pairs, C5
-65536), distinct seeded data per rank, per-GPU work fixed as N grows.  ``--scaling strong``
-splits the config's batch B into contiguous per-rank blocks (wtmi.sharding.shard_range)
-instead (the shard-size measurements).  ``--gpus N`` works two ways:
+timed region.  The default scaling mode follows BASELINE's wording of each config
+(DEFAULT_SCALING): C4 ("512 series pairs ... sharded by pair 1->8 GPUs") and C5 ("65536 series
+... sharded across 8xMI355X") are fixed totals, so ``--scaling strong`` splits the config's
+batch B into contiguous per-rank blocks (wtmi.sharding.shard_range); C2 and C3 are single-GPU
+configs, so at N > 1 ``--scaling weak`` gives rank r its own block [r B, (r + 1) B) of a global
+batch of N B series (distinct seeded data per rank, per-GPU work fixed as N grows).  Either
+mode can be forced.  The JSON carries each rank's own time for its K steps (min / max over
+ranks) and the closing barrier's wait beside the max-over-ranks total.  ``--plan-only`` prints
+the ranks' row ranges without touching a GPU.  ``--gpus N`` works two ways:
   * under ``torch.distributed.run --nproc-per-node N`` (RANK/WORLD_SIZE in the env):
     this process is one rank; ``--gpus`` must equal WORLD_SIZE;
   * as a plain ``python bench.py --gpus N``: this process starts N fresh rank processes
