@@ -199,8 +199,7 @@ int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batc
  * rows, 0 full transforms), wct_target_wg, wct_min_rows and wct_dec_rows (scale rows per WCT
  * workgroup and decimated rows per phase-A workgroup; 0 = chosen by batch size), modwt_syn
  * (n = 8192 / 16384 synthesis: 1 hybrid kernel with the low levels staged through LDS, 0
- * dilation chains only), modwt_bufst (n = 16384 analysis: 1 W_j stores through a buffer
- * descriptor, 0 global stores), wct_wide (0: windows touching a full-band row always take the
+ * dilation chains only), wct_wide (0: windows touching a full-band row always take the
  * time-domain path; 1..3: from which union-band exponent on they take the spectral route),
  * wct_side_stream (1: the full-band rows' kernel on a pooled side stream beside the
  * decimated rows' chain).  The prune and kernel switches exist so that tests can

@@ -170,8 +170,6 @@ struct Options {
   int modwt_syn = 1;        // WTMI_MODWT_SYN: 1 hybrid synthesis (low levels via LDS), 0 MODE 3 only
   int wct_wide = 1;         // WTMI_WCT_WIDE: windows of union band N >> e take the spectral route
                             // from e >= wct_wide (1..3); 0 = never (time path)
-  int modwt_bufst = 0;      // WTMI_MODWT_BUFST: n = 16384 analysis W_j stores through a buffer
-                            // descriptor (1) or global stores (0)
   int wct_side_stream = 1;  // WTMI_WCT_SIDE_STREAM: full-band rows on a side stream beside the
                             // decimated rows' chain (1), or all on the caller's stream (0)
 };

@@ -304,9 +304,7 @@ __device__ __forceinline__ void fma4(float4& acc, float c, const float4& s) {
 // mapping of syn_level_chain (taps m-L+1 .. m of the thread's chain, M+L-1 LDS reads for
 // M outputs instead of L*M); W_j stores then run along the chain (coalesced for
 // dq >= 64 groups, dq-group runs below: whole 128-byte lines from dq = 8).
-// BUFST: W_j stores through a wave-uniform buffer descriptor of the row (one 32-bit offset
-// VGPR per store instead of a 64-bit address pair; option modwt_bufst).
-template <int L, int GROUPS, int T, int CHAIN = 0, bool BUFST = false>
+template <int L, int GROUPS, int T, int CHAIN = 0>
 __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ x, long long ld,
                                                       int n, int level, FilterBank fb,
                                                       float* __restrict__ w) {
@@ -330,14 +328,6 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
   for (int j = 1; j <= level; ++j) {
     const int dm = dilation_mod(j, n);
     float4* wrow = reinterpret_cast<float4*>(wout + static_cast<long long>(j - 1) * n);
-    __amdgpu_buffer_rsrc_t wr;
-    if constexpr (BUFST) wr = uniform_rsrc(wrow);
-    auto put = [&](int q, const float4& v) {
-      if constexpr (BUFST)
-        buf_st(v, wr, 16 * q, 0);
-      else
-        wrow[q] = v;
-    };
     int tl = tid;
     asm volatile("" : "+v"(tl));
     float4 vreg[GROUPS];
@@ -358,7 +348,7 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
             fma4(aw, fb.h[l], vv[m + L - 1 - l]);
             fma4(av, fb.g[l], vv[m + L - 1 - l]);
           }
-          put(q0 + m * dq, aw);
+          wrow[q0 + m * dq] = aw;
           vreg[m] = av;
           pin4(vreg[m]);
         }
@@ -391,7 +381,7 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
           fma4(av, fb.g[l], s);
         }
       }
-      if (tl + k * T < ng) put(q, aw);
+      if (tl + k * T < ng) wrow[q] = aw;
       vreg[k] = av;
       pin4(vreg[k]);
     }
@@ -924,12 +914,7 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
       launch(modwt_vec_kernel<8, 2, 1024>, 1024);
     else  // chains from dq >= 16 groups; one-process A/B on two boxes (ms): stride form 1.248 /
           // 1.264, chains from dq 8 1.200 / 1.264, from dq 16 1.200 / 1.267 (r01)
-    {
-      if (options().modwt_bufst)
-        launch(modwt_vec_kernel<8, 8, 512, 16, true>, 512);
-      else
-        launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
-    }
+      launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
   } else if (n_taps == 8) {
     allow_lds(modwt_kernel<8>, lds);
     hipLaunchKernelGGL(modwt_kernel<8>, dim3(batch), dim3(block), lds, st, x, ld, ni, level, n_taps, fb, w);

@@ -20,7 +20,6 @@ constexpr Entry kEntries[] = {
     {"wct_min_rows", &Options::wct_min_rows, 0, 1 << 10},
     {"wct_dec_rows", &Options::wct_dec_rows, 0, 128},
     {"modwt_syn", &Options::modwt_syn, 0, 1},
-    {"modwt_bufst", &Options::modwt_bufst, 0, 1},
     {"wct_wide", &Options::wct_wide, 0, 4},
     {"wct_side_stream", &Options::wct_side_stream, 0, 1},
 };
@@ -58,7 +57,7 @@ const Options& options() { return thread_options(); }
 }  // namespace wtmi
 
 // Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
-// wct_min_rows, wct_dec_rows, modwt_syn, modwt_bufst, wct_wide, wct_side_stream) for the CALLING
+// wct_min_rows, wct_dec_rows, modwt_syn, wct_wide, wct_side_stream) for the CALLING
 // thread.  0 on success, -1 unknown
 // name or out of range.  Applies to launches this thread issues after the call; other
 // threads keep their own values (the process defaults come from WTMI_<NAME>).
