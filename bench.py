@@ -416,9 +416,10 @@ CONFIGS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5, "stub": Stub}
 # sharded by pair 1->8 GPUs") and C5 ("65536 series ... sharded across 8xMI355X") name a FIXED
 # total batch split over the GPUs -- strong scaling; C2 and C3 are single-GPU configs, so at
 # N > 1 every GPU runs the whole config on its own series -- weak scaling.
-# hipGraph replay of the step by default where it pays: strong-scaling shards of C4 are
-# launch-bound (a dozen launches + the side-stream fork / join per step)
-DEFAULT_GRAPH = {"c4": 1}
+# hipGraph replay of the step (--graph 1): measured no faster for any config, C4's shards
+# included (profiles/r04/shard_sizes.txt: the kernels' own tails, not the host's launches, cost
+# the small-batch efficiency), so no config uses it by default
+DEFAULT_GRAPH: dict = {}
 DEFAULT_SCALING = {"c2": "weak", "c3": "weak", "c4": "strong", "c5": "strong", "stub": "weak"}
 
 

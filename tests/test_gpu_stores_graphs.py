@@ -43,7 +43,7 @@ def _scales(n0, dj, S):
     return torch.tensor(sj, device="cuda", dtype=torch.float64)
 
 
-@pytest.mark.parametrize("n0", [100, 700, 1333, 5000, 12000])
+@pytest.mark.parametrize("n0", [100, 700, 1333, 5000, 12000, 20000])
 def test_cwt_xwt_padded_rows_write_only_their_samples(n0):
     from wtmi import _lib, ops
     from wtmi.ops import _ptr, _stream
@@ -56,8 +56,13 @@ def test_cwt_xwt_padded_rows_write_only_their_samples(n0):
     nf = B * S * n0
     bw, bp, bs = _sentinel(2 * nf), _sentinel(nf), _sentinel(nf)
     dev = x1.device
+
+    def ws(pair):  # rows above 16384 samples run the four-step path through a workspace
+        need = ops.cwt_workspace_bytes(B, n0, S, pair)
+        return torch.empty(need, dtype=torch.uint8, device="cuda") if need else None
+
     _lib.call("wtmi_cwt_mother", _ptr(x1), x1.stride(0), B, n0, None, _ptr(sj), S, 1 / 12, 0, 6.0,
-              _ptr(sig), 0, _ptr(bw), _ptr(bp), _ptr(bs), None, _stream(dev))
+              _ptr(sig), 0, _ptr(bw), _ptr(bp), _ptr(bs), _ptr(ws(False)), _stream(dev))
     torch.cuda.synchronize()
     assert _tail_ok(bw, 2 * nf) and _tail_ok(bp, nf) and _tail_ok(bs, nf)
     assert torch.equal(bw[:2 * nf].view(torch.complex64).view(B, S, n0), ref["w"])
@@ -68,7 +73,7 @@ def test_cwt_xwt_padded_rows_write_only_their_samples(n0):
                         want_sig=True, want_uv=True)
     bufs = [_sentinel(2 * nf)] + [_sentinel(nf) for _ in range(4)]
     _lib.call("wtmi_xwt_mother", _ptr(x1), _ptr(x2), x1.stride(0), B, n0, None, None, _ptr(sj), S,
-              1 / 12, 0, 6.0, _ptr(sig), 0, *[_ptr(b) for b in bufs], None, _stream(dev))
+              1 / 12, 0, 6.0, _ptr(sig), 0, *[_ptr(b) for b in bufs], _ptr(ws(True)), _stream(dev))
     torch.cuda.synchronize()
     assert _tail_ok(bufs[0], 2 * nf) and all(_tail_ok(b, nf) for b in bufs[1:])
     assert torch.equal(bufs[0][:2 * nf].view(torch.complex64).view(B, S, n0), rx["w12"])
@@ -76,7 +81,8 @@ def test_cwt_xwt_padded_rows_write_only_their_samples(n0):
         assert torch.equal(b[:nf].view(B, S, n0), rx[k]), k
 
 
-@pytest.mark.parametrize("n0,dj", [(100, 1 / 8), (1333, 1 / 8), (5000, 1 / 8), (12000, 1 / 12)])
+@pytest.mark.parametrize("n0,dj", [(100, 1 / 8), (1333, 1 / 8), (5000, 1 / 8), (12000, 1 / 12),
+                                  (20000, 1 / 4)])
 def test_wct_padded_rows_write_only_their_samples(n0, dj):
     from wtmi import _lib, ops, transforms
     from wtmi.ops import _ptr, _stream
@@ -87,13 +93,18 @@ def test_wct_padded_rows_write_only_their_samples(n0, dj):
     S = sj_h.size
     sj = torch.tensor(sj_h, device="cuda")
     K = transforms.boxcar_rows(transforms.as_morlet(None), dj)
+    norm = n0 <= 16384  # pycwt's normalisation in the first kernel (FFT rows); raw above
     ref = ops.wct_morlet(y1, y2, sj, 1 / 12, boxcar=K, want_uv=True, want_power=True,
-                         want_phase=True, normalize=True)
+                         want_phase=True, normalize=norm)
     nf = B * S * n0
     bufs = [_sentinel(nf) for _ in range(5)]
     ws = torch.empty(ops.wct_workspace_bytes(B, n0, S), dtype=torch.uint8, device="cuda")
-    _lib.call("wtmi_wct_morlet_norm", _ptr(y1), _ptr(y2), y1.stride(0), B, n0, _ptr(sj), S, 1 / 12, 6.0,
-              K, _ptr(ws), *[_ptr(b) for b in bufs], _stream(y1.device))
+    if norm:
+        _lib.call("wtmi_wct_morlet_norm", _ptr(y1), _ptr(y2), y1.stride(0), B, n0, _ptr(sj), S, 1 / 12, 6.0,
+                  K, _ptr(ws), *[_ptr(b) for b in bufs], _stream(y1.device))
+    else:
+        _lib.call("wtmi_wct_morlet", _ptr(y1), _ptr(y2), y1.stride(0), B, n0, None, None, _ptr(sj), S,
+                  1 / 12, 6.0, K, _ptr(ws), *[_ptr(b) for b in bufs], _stream(y1.device))
     torch.cuda.synchronize()
     for b, k in zip(bufs, ("coh", "power", "phase", "u", "v")):
         assert _tail_ok(b, nf), k

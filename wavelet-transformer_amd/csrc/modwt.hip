@@ -914,7 +914,14 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
       launch(modwt_vec_kernel<8, 2, 1024>, 1024);
     else  // chains from dq >= 16 groups; one-process A/B on two boxes (ms): stride form 1.248 /
           // 1.264, chains from dq 8 1.200 / 1.264, from dq 16 1.200 / 1.267 (r01)
-      launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
+    {
+      if (options().modwt_ana == 1)
+        launch(modwt_vec_kernel<8, 4, 1024, 16>, 1024);
+      else if (options().modwt_ana == 2)
+        launch(modwt_vec_kernel<8, 16, 256, 16>, 256);
+      else
+        launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
+    }
   } else if (n_taps == 8) {
     allow_lds(modwt_kernel<8>, lds);
     hipLaunchKernelGGL(modwt_kernel<8>, dim3(batch), dim3(block), lds, st, x, ld, ni, level, n_taps, fb, w);

@@ -1602,16 +1602,22 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
 
 // Phase C over the chunk grid phase A used (a.nchunks / a.chunk as launch_phase_a set them).
 template <int LOGN>
+// which: 1 the q windows, 2 the wide windows, 3 both (in that order).
 static int launch_phase_c(const CwtArgs& a, const cpx* SB, const cpx* WB, const int* plan, int K, float* coh,
-                          hipStream_t st) {
+                          hipStream_t st, int which = 3) {
   using G = WctGeom<LOGN>;
   const dim3 gd(static_cast<unsigned>(a.batch * a.nchunks));
-  if (a.n0 == (1 << LOGN))
-    hipLaunchKernelGGL((wct_phase_c<LOGN, true, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
-  else
-    hipLaunchKernelGGL((wct_phase_c<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
-  int rc = launch_status();
-  if (rc != kOk || LOGN < kWideMinLogn || a.prune < 1 || options().wct_wide < 1 || K > kWideMaxK) return rc;
+  int rc = kOk;
+  if (which & 1) {
+    if (a.n0 == (1 << LOGN))
+      hipLaunchKernelGGL((wct_phase_c<LOGN, true, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
+    else
+      hipLaunchKernelGGL((wct_phase_c<LOGN, false, false>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
+    rc = launch_status();
+  }
+  if (!(which & 2) || rc != kOk || LOGN < kWideMinLogn || a.prune < 1 || options().wct_wide < 1 ||
+      K > kWideMaxK)
+    return rc;
   if (a.n0 == (1 << LOGN))
     hipLaunchKernelGGL((wct_phase_c<LOGN, true, true>), gd, dim3(G::BLOCK), 0, st, a, SB, WB, plan, K, coh);
   else
@@ -1915,9 +1921,9 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
   }
   if (rc != kOk) return rc;
   const int n0i = static_cast<int>(n0);
-  auto phase_c = [&](hipStream_t cs) -> int {
+  auto phase_c = [&](hipStream_t cs, int which) -> int {
     switch (logn) {
-#define WTMI_C(L) case L: return launch_phase_c<L>(a, SB, WB, plan, boxcar, out_coh, cs);
+#define WTMI_C(L) case L: return launch_phase_c<L>(a, SB, WB, plan, boxcar, out_coh, cs, which);
       WTMI_C(4) WTMI_C(5) WTMI_C(6) WTMI_C(7) WTMI_C(8) WTMI_C(9) WTMI_C(10) WTMI_C(11)
       WTMI_C(12) WTMI_C(13) WTMI_C(14)
 #undef WTMI_C
@@ -1929,9 +1935,18 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
   // which the side stream made, and of the decimated rows), while phase B runs here once the
   // full-band rows' time-domain rows are done; the caller's stream then joins the side stream.
   hipStream_t sc = st;
+  // option wct_pc_early: phase C's q windows on a third (pooled) stream as soon as the
+  // decimated spectra are done -- every row of a q window is a decimated row, so they need
+  // neither the full-band rows' kernel nor the spectral boxcar
+  SideJoin sj3(side && options().wct_pc_early, st);
   if (side) {
     if (hipStreamWaitEvent(side->s, side->dec, 0) != hipSuccess) return launch_status();
     sc = side->s;
+    if (sj3.side) {
+      if (hipStreamWaitEvent(sj3.side->s, side->dec, 0) != hipSuccess) return launch_status();
+      sj3.forked = true;
+      if ((rc = phase_c(sj3.side->s, 1)) != kOk) return rc;
+    }
   }
   // spectral boxcar of the wide windows (their sums over the output rows' WB slots)
   if (wct_wb_bytes(batch, n0, n_scales) > 0 && a.prune >= 1 && boxcar <= kWideMaxK) {
@@ -1951,7 +1966,7 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
     }
     if ((rc = launch_status()) != kOk) return rc;
   }
-  if ((rc = phase_c(sc)) != kOk) return rc;
+  if ((rc = phase_c(sc, sj3.side ? 2 : 3)) != kOk) return rc;
   // phase B on the caller's stream once the full-band rows are done; sj joins the side stream
   if (side && hipStreamWaitEvent(st, side->k0, 0) != hipSuccess) return launch_status();
   return wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st);
