@@ -45,7 +45,11 @@ __device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, 
       ru = uniform_rsrc(pu_, n4);
       rv = uniform_rsrc(pv_, n4);
     }
-    auto vo = [&](int m, int sz) { return (FULL || t + m * P::NT < a.n0) ? sz * t : sz * a.n0; };
+    // (the selects depend only on t and n0: an opaque copy of t keeps the compiler from
+    // hoisting all 16 out of the scale loop -- 16 live VGPRs, 108 spilled bytes at LOGN 13)
+    int tt = t;
+    if constexpr (!FULL) asm volatile("" : "+v"(tt));
+    auto vo = [&](int m, int sz) { return (FULL || tt + m * P::NT < a.n0) ? sz * t : sz * a.n0; };
 #pragma unroll
     for (int m = 0; m < 16; ++m)
       if constexpr (KIND & kOutW) buf_st(v[m], rw, vo(m, 8), 8 * m * P::NT);

@@ -137,9 +137,11 @@ __device__ __forceinline__ void put_row(T* row, int t, int n0, F&& val) {
 #pragma unroll
       for (int m = 0; m < 16; ++m) buf_st(val(m), r, SZ * t, SZ * m * P::NT);
     } else {
+      int tt = t;  // per row, not hoisted out of the caller's row loop (16 live selects)
+      asm volatile("" : "+v"(tt));
 #pragma unroll
       for (int m = 0; m < 16; ++m)
-        buf_st(val(m), r, t + m * P::NT < n0 ? SZ * t : SZ * n0, SZ * m * P::NT);
+        buf_st(val(m), r, tt + m * P::NT < n0 ? SZ * t : SZ * n0, SZ * m * P::NT);
     }
   } else {
 #pragma unroll
