@@ -170,10 +170,11 @@ struct Options {
   int modwt_syn = 1;        // WTMI_MODWT_SYN: 1 hybrid synthesis (low levels via LDS), 0 MODE 3 only
   int wct_wide = 1;         // WTMI_WCT_WIDE: windows of union band N >> e take the spectral route
                             // from e >= wct_wide (1..3); 0 = never (time path)
-  int modwt_ana = 0;        // WTMI_MODWT_ANA (A/B): n = 16384 analysis with 512 threads x 8 groups (0),
-                            // 1024 x 4 (1) or 256 x 16 (2)
-  int wct_pc_early = 0;     // WTMI_WCT_PC_EARLY (A/B): phase C's q windows on a third stream right
-                            // after the decimated spectra (1), or after the full-band rows (0)
+  int modwt_ana = 0;        // WTMI_MODWT_ANA: n = 16384 analysis with 1024 threads x 4 groups (0),
+                            // 512 x 8 (1, r01-r03) or 256 x 16 (2)
+  int wct_pc_early = 2;     // WTMI_WCT_PC_EARLY: phase C's q windows on a third stream right after
+                            // the decimated spectra (1), after the full-band rows (0), or the
+                            // former for batches of at most 256 pairs (2)
   int wct_side_stream = 1;  // WTMI_WCT_SIDE_STREAM: full-band rows on a side stream beside the
                             // decimated rows' chain (1), or all on the caller's stream (0)
 };

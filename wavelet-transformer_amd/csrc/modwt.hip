@@ -915,12 +915,15 @@ extern "C" int wtmi_modwt(const float* x, long long ld, long long batch, long lo
     else  // chains from dq >= 16 groups; one-process A/B on two boxes (ms): stride form 1.248 /
           // 1.264, chains from dq 8 1.200 / 1.264, from dq 16 1.200 / 1.267 (r01)
     {
+      // one 1024-thread workgroup per series (4 groups per thread): 1.256 ms against 1.280 for
+      // 512 threads x 8 groups and 1.263 for 256 x 16 (C3's analysis, alternating, one box,
+      // r04); option modwt_ana = 1 / 2 selects the others
       if (options().modwt_ana == 1)
-        launch(modwt_vec_kernel<8, 4, 1024, 16>, 1024);
+        launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
       else if (options().modwt_ana == 2)
         launch(modwt_vec_kernel<8, 16, 256, 16>, 256);
       else
-        launch(modwt_vec_kernel<8, 8, 512, 16>, 512);
+        launch(modwt_vec_kernel<8, 4, 1024, 16>, 1024);
     }
   } else if (n_taps == 8) {
     allow_lds(modwt_kernel<8>, lds);

@@ -1424,7 +1424,8 @@ static int wct_min_rows(long long batch) {
 }
 static int wct_dec_rows_per_wg(long long batch) {
   const int o = options().wct_dec_rows;
-  return o > 0 ? o : (batch <= 256 ? 8 : 4);
+  // 64 pairs (r04, alternating): 8 rows 0.492 ms, 6 0.487, 4 0.486, 3 0.487, 2 0.489
+  return o > 0 ? o : (batch <= 64 ? 4 : batch <= 256 ? 8 : 4);
 }
 
 // Side streams for the full-band rows' kernel beside the decimated rows' chain (fork after the
@@ -1939,8 +1940,11 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
   hipStream_t sc = st;
   // option wct_pc_early: phase C's q windows on a third (pooled) stream as soon as the
   // decimated spectra are done -- every row of a q window is a decimated row, so they need
-  // neither the full-band rows' kernel nor the spectral boxcar
-  SideJoin sj3(side && options().wct_pc_early, st);
+  // neither the full-band rows' kernel nor the spectral boxcar.  A/B (alternating, one box,
+  // r04): 64 pairs 0.495 -> 0.482 ms, 128 pairs 0.843 -> 0.831, 512 pairs 3.039 -> 3.053, so
+  // by default (2) for batches of at most 256 pairs
+  const int pce = options().wct_pc_early;
+  SideJoin sj3(side && (pce == 1 || (pce == 2 && batch <= 256)), st);
   if (side) {
     if (hipStreamWaitEvent(side->s, side->dec, 0) != hipSuccess) return launch_status();
     sc = side->s;
