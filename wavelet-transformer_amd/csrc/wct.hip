@@ -809,6 +809,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   const int g = tid / P::NT;
   const int t = fft_thread<LOGN>(tid - g * P::NT);
   // the scale chunks of one pair share its two spectra: keep them on one XCD's L2
+  // (chunk-major order for the decimated rows, costliest chunks first, measured neutral: r04)
   const long long blk = xcd_remap(blockIdx.x, gridDim.x);
   const long long b = blk / a.nchunks;
   const int ch = static_cast<int>(blk - b * a.nchunks);
