@@ -203,7 +203,9 @@ int wtmi_series_affine(const void* x, int x_is_f64, long long ld, long long batc
  * time-domain path; 1..3: from which union-band exponent on they take the spectral route),
  * wct_side_stream (1: the full-band rows' kernel on a pooled side stream beside the
  * decimated rows' chain), wct_pc_early (phase C's q windows on a third pooled stream right
- * after the decimated spectra: 1 always, 0 never, 2 for batches of at most 256 pairs), modwt_ana
+ * after the decimated spectra: 1 always, 0 never, 2 for batches of at most 256 pairs),
+ * wct_dec_merge (the decimation classes M = 4096 .. 512 in one launch: 1 always, 0 never, 2 for
+ * batches of at most 256 pairs), modwt_ana
  * (n = 16384 analysis geometry: 0 1024 threads x 4 float4 groups, 1 512 x 8, 2 256 x 16).  The prune and kernel switches exist so that tests can
  * compare the paths; results agree to fp32 resolution either way.  The environment gives the process
  * defaults; wtmi_set_option changes the CALLING thread's value only (thread-local), so it

@@ -27,6 +27,7 @@ BUDGET = {
     "void wtmi::imodwt_hyb_kernel<8, 8, 512, 2, 4>": 128,  # C3 synthesis: two workgroups / CU
 }
 BUDGET.update({f"void wtmi::wct_dec_kernel<13, {m}>": 128 for m in range(8, 13)})
+BUDGET["void wtmi::wct_dec_merged<13>"] = 128  # C4 decimation classes M = 4096 .. 512, one launch
 
 
 @pytest.fixture(scope="module")

@@ -177,6 +177,9 @@ struct Options {
                             // former for batches of at most 256 pairs (2)
   int wct_side_stream = 1;  // WTMI_WCT_SIDE_STREAM: full-band rows on a side stream beside the
                             // decimated rows' chain (1), or all on the caller's stream (0)
+  int wct_dec_merge = 2;    // WTMI_WCT_DEC_MERGE: the decimation classes M = 4096 .. 512 in one
+                            // launch (1), one launch per class (0), or the former for batches of
+                            // at most 256 pairs (2)
 };
 const Options& options();
 

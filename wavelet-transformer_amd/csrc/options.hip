@@ -24,6 +24,7 @@ constexpr Entry kEntries[] = {
     {"wct_wide", &Options::wct_wide, 0, 4},
     {"wct_side_stream", &Options::wct_side_stream, 0, 1},
     {"wct_pc_early", &Options::wct_pc_early, 0, 2},
+    {"wct_dec_merge", &Options::wct_dec_merge, 0, 2},
 };
 
 // Process defaults: the environment, read once (immutable afterwards).
@@ -59,7 +60,8 @@ const Options& options() { return thread_options(); }
 }  // namespace wtmi
 
 // Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
-// wct_min_rows, wct_dec_rows, modwt_syn, modwt_ana, wct_wide, wct_side_stream, wct_pc_early) for the CALLING
+// wct_min_rows, wct_dec_rows, modwt_syn, modwt_ana, wct_wide, wct_side_stream, wct_pc_early,
+// wct_dec_merge) for the CALLING
 // thread.  0 on success, -1 unknown
 // name or out of range.  Applies to launches this thread issues after the call; other
 // threads keep their own values (the process defaults come from WTMI_<NAME>).

@@ -1049,6 +1049,48 @@ __global__ void __launch_bounds__(512, 4) wct_dec_kernel(CwtArgs a, const cpx* _
 }
 
 
+// The grid-stride classes (M = 2^12 .. 2^9) in ONE launch: the schedule numbers their
+// workgroup items consecutively, largest M first, so a block striding over [0, w(M = 256))
+// finds its class by comparing with the classes' first items.  Four launches' ramp and drain
+// fewer on the decimated chain (a strong-scaling shard's kernels are short).  Every class has
+// the same workgroup shape (512 threads) and LDS size (2 x 8448 complex).
+template <int LOGN>
+__global__ void __launch_bounds__(512, 4) wct_dec_merged(CwtArgs a, const cpx* __restrict__ spec,
+                                                         cpx* __restrict__ TA, cpx* __restrict__ TB,
+                                                         cpx* __restrict__ SB, cpx* __restrict__ DY,
+                                                         cpx* __restrict__ WB, const int* __restrict__ plan) {
+  constexpr int kTop = LOGN - dec_min_e<LOGN>() < kDecMaxLogm ? LOGN - dec_min_e<LOGN>() : kDecMaxLogm;
+  __shared__ cpx lds[2 * dec_rows_per_wg(kDecMaxLogm) * FftPlan<kDecMaxLogm>::PADN];
+  static_assert(dec_rows_per_wg(kDecStrideLogm) * FftPlan<kDecStrideLogm>::PADN <=
+                    dec_rows_per_wg(kDecMaxLogm) * FftPlan<kDecMaxLogm>::PADN, "LDS of the merged classes");
+  const int* rows = plan + 3 * a.S + 1;
+  const int* sched = rows + a.S;
+  const int end = sched[4 * (kDecStrideLogm - 1) + 2];  // first item of M = 256
+  for (int wl = blockIdx.x; wl < end; wl += gridDim.x) {
+    if (wl != static_cast<int>(blockIdx.x)) __syncthreads();  // the previous item's LDS reads are done
+#define WTMI_DM(LM)                                                                         \
+  if constexpr (LM <= kTop) {                                                               \
+    if (wl < (LM > kDecStrideLogm ? sched[4 * (LM - 1) + 2] : end)) {                       \
+      dec_items<LOGN, LM>(a, spec, TA, TB, SB, DY, WB, plan, rows, sched, wl - sched[4 * LM + 2], lds); \
+      continue;                                                                             \
+    }                                                                                       \
+  }
+    WTMI_DM(12) WTMI_DM(11) WTMI_DM(10) WTMI_DM(9)
+#undef WTMI_DM
+  }
+}
+
+template <int LOGN>
+static int launch_dec_merged(const CwtArgs& a, const cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY,
+                             cpx* WB, const int* plan, hipStream_t st) {
+  long long most = 0;  // the classes' workgroup items are at most this many
+  for (int lm = kDecStrideLogm; lm <= kDecMaxLogm; ++lm)
+    most += (a.batch * a.S + dec_rows_per_wg(lm) - 1) / dec_rows_per_wg(lm);
+  const unsigned dg = static_cast<unsigned>(most < kDecGrid ? most : kDecGrid);
+  hipLaunchKernelGGL((wct_dec_merged<LOGN>), dim3(dg), dim3(512), 0, st, a, spec, TA, TB, SB, DY, WB, plan);
+  return launch_status();
+}
+
 template <int LOGN, int LOGM>
 static int launch_dec_class(const CwtArgs& a, const cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx* DY,
                             cpx* WB, const int* plan, hipStream_t st) {
@@ -1419,9 +1461,14 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
 // (wct_dec_rows; one box, two alternations, ms): 64 pairs (min 1, dec 2) 0.524-0.549 -> (1, 4)
 // 0.516-0.520 or (1, 8) 0.519-0.521; 128 (1, 2) 0.959-0.962 -> (2, 8) 0.924-0.927; 256 (2, 2)
 // 1.729-1.730 -> (2, 8) 1.694-1.697; 512 (4, 4) 3.227-3.236, (4, 8) 3.253-3.262, (2, 8) 3.34-3.38.
+// r04 re-sweep after the merged decimation launch and phase C's third stream (one box,
+// alternating in one process, ms for min rows 1 / 2 / 3 / 4): 64 pairs 0.458 / 0.450 / 0.449 /
+// 0.449, 128 pairs 0.870 / 0.826 / 0.818 / 0.802, 256 pairs 1.656 / 1.635 / 1.637 / 1.562, 512
+// pairs 3.235 / 3.132 / 3.106 / 3.073: four rows per workgroup at every batch.
 static int wct_min_rows(long long batch) {
+  (void)batch;
   const int o = options().wct_min_rows;
-  return o > 0 ? o : (batch <= 64 ? 1 : batch <= 256 ? 2 : 4);
+  return o > 0 ? o : 4;
 }
 static int wct_dec_rows_per_wg(long long batch) {
   const int o = options().wct_dec_rows;
@@ -1581,7 +1628,16 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
   }
   if constexpr (LOGN >= kDecMinLogn) {
     if (dec) {
-      for (int lm = kDecMaxLogm; lm >= kDecEngLogm; --lm) {
+      // one launch for the grid-stride classes: A/B (alternating, one box, r04) 64 pairs
+      // 0.492 -> 0.459 ms, 128 pairs 0.846 -> 0.821, 512 pairs 3.11 -> 3.20, so by default (2)
+      // for batches of at most 256 pairs
+      const int dm = options().wct_dec_merge;
+      const bool merged = dm == 1 || (dm == 2 && a.batch <= 256);
+      if (merged) {
+        if ((rc = launch_dec_merged<LOGN>(a, spec, TA, TB, SB, DY, WB, plan, st)) != kOk) return rc;
+        if ((rc = launch_dec_class<LOGN, kDecEngLogm>(a, spec, TA, TB, SB, DY, WB, plan, st)) != kOk) return rc;
+      }
+      for (int lm = kDecMaxLogm; lm >= kDecEngLogm && !merged; --lm) {
         switch (lm) {
 #define WTMI_DC(LM) case LM: rc = launch_dec_class<LOGN, LM>(a, spec, TA, TB, SB, DY, WB, plan, st); break;
           WTMI_DC(12) WTMI_DC(11) WTMI_DC(10) WTMI_DC(9) WTMI_DC(8)
