@@ -292,11 +292,17 @@ __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16]
 //                   (eu in 1..3: the window holds rows of regime q = 0 but none of band ew = 0),
 //                   its coherence comes from the WB spectra through one band inverse of Mu bins
 //                   per field instead of the time-domain workspace
+//   bits 18-21 ec   q-window output row (qw >= 1): the union of its window rows' smoothed bands
+//                   is Mc = N >> ec (ec >= 4 qw: the smallest ew of the window, at least the
+//                   regime's band), so phase C's band inverses enter at pass ec / 4 with
+//                   16 >> (ec % 4) non-zero inputs per thread
 enum : int { kPlanQ = 3, kPlanNeedT = 4, kPlanNeedS = 8, kPlanSpec = 16, kPlanQwShift = 5,
-             kPlanNeedW = 128, kPlanDecShift = 8, kPlanEwShift = 12, kPlanEuShift = 16 };
+             kPlanNeedW = 128, kPlanDecShift = 8, kPlanEwShift = 12, kPlanEuShift = 16,
+             kPlanEcShift = 18 };
 __device__ __forceinline__ int plan_dec(int pl) { return (pl >> kPlanDecShift) & 15; }
 __device__ __forceinline__ int plan_ew(int pl) { return (pl >> kPlanEwShift) & 15; }
 __device__ __forceinline__ int plan_eu(int pl) { return (pl >> kPlanEuShift) & 3; }
+__device__ __forceinline__ int plan_ec(int pl) { return (pl >> kPlanEcShift) & 15; }
 // wide windows need M = N >> 3 >= 32 bins (one band phasor per thread): LOGN >= 8; the
 // spectral boxcar keeps K rows in registers: K <= 24
 constexpr int kWideMinLogn = 8;
@@ -382,7 +388,9 @@ __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales,
     const int q_ok = (prune && qw >= 1) ? qw : -1;
     const int eu = (prune && kWide && wide >= 1 && K <= kWideMaxK && q_ok < 1 && ew >= wide)
                        ? min(ew, kWideMaxE) : 0;
-    qwin[i] = (q_ok >= 1 ? q_ok : 0) | (eu << 4);
+    // q windows: the union band of the smoothed rows (never wider than the regime's band)
+    const int ec = q_ok >= 1 ? max(4 * q_ok, min(ew, LOGN - 5)) : 0;
+    qwin[i] = (q_ok >= 1 ? q_ok : 0) | (eu << 4) | (ec << 8);
   }
   __syncthreads();
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
@@ -394,10 +402,10 @@ __device__ __forceinline__ void wct_plan_body(const double* __restrict__ scales,
       else if (eui >= 1) needW = true;
       else needT = true;
     }
-    const int qw = qwin[r] & 15, eu = (qwin[r] >> 4) & 3;
+    const int qw = qwin[r] & 15, eu = (qwin[r] >> 4) & 3, ec = (qwin[r] >> 8) & 15;
     plan[r] = q | (needT ? kPlanNeedT : 0) | (needS && q >= 1 ? kPlanNeedS : 0) |
               (needW ? kPlanNeedW : 0) |
-              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) : 0) |
+              (qw >= 1 ? kPlanSpec | (qw << kPlanQwShift) | (ec << kPlanEcShift) : 0) |
               (eu >= 1 ? kPlanSpec | (eu << kPlanEuShift) : 0) |
               (e << kPlanDecShift) | (ew << kPlanEwShift);
     if (qw < 1 && eu < 1) atomicMax(&last, r);
@@ -1224,14 +1232,49 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
 //   S1 + i S2 = IFFT(sum_q w_q Z_q),   S12 = IFFT(sum_q w_q W_q),   WCT = |S12|^2 / (S1 S2).
 // These rows skip the time-domain workspace (16 B per coefficient written by phase A and
 // read back by phase B) and phase A's smoothing transforms move here.
-template <int LOGN, int Q, bool BUF, bool TWL, bool FULL>
+// EC (r04, plan bits ec): the window's rows have their smoothed spectra in [-Mc/2, Mc/2), Mc =
+// N >> EC, so the sums are exchanged shifted by Mc/2 (not by the regime band's half width) and
+// the inverse transforms enter at pass EC / 4 with 16 >> (EC % 4) non-zero inputs per thread
+// (BandGeom, as the decimated rows' band inverses); the shift's time phasor has H = Mc/2.
+template <int LOGN, int EC>
+__host__ __device__ constexpr bool spec_ec_ok() {
+  using P = FftPlan<LOGN>;
+  return EC >= 4 && EC <= LOGN - 5 && EC / 4 < P::P16 && (P::NT % (1 << (4 * (EC / 4)))) == 0 &&
+         (P::N >> EC) >= 32;
+}
+
+// Smoothed row from the window sum of its band bin: band exchange of Mc = N >> EC shifted bins,
+// inverse FFT from pass EC / 4 over the NZ non-zero inputs, time phasor exp(-2 pi i (Mc/2) n / N).
+template <int LOGN, int EC, bool TWL, bool PHASOR = true>
+__device__ __forceinline__ void smooth_from_band_ec(cpx (&v)[16], cpx y, int slot, cpx* my, const cpx* tw,
+                                                    int t, int& par, const float4* twl) {
+  using P = FftPlan<LOGN>;
+  using BG = BandGeom<LOGN, EC>;
+  constexpr int STEP = P::NT >> (4 * BG::Q);
+  __syncthreads();
+  if (slot >= 0) my[slot] = y;
+  __syncthreads();
+  const int base = t >> (4 * BG::Q);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = r < BG::NZ ? my[base + r * STEP] : mkc(0.f, 0.f);
+  fft_row<LOGN, 1, 1, TWL, BG::Q, BG::NZ>(v, my, 0, tw, t, par, twl);
+  if constexpr (PHASOR) {
+    int tt = t;
+    asm volatile("" : "+v"(tt));  // per row, not hoisted (register budget)
+    const cpx ph = expi_frac(-BG::H * tt, P::N);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = cmul2(v[m], ph);
+  }
+}
+
+template <int LOGN, int EC, bool BUF, bool TWL, bool FULL>
 __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __restrict__ SB, int K,
                                               long long b, int j0, int r0, int r1, cpx* my, const cpx* tw,
                                               int g, int t, int& par, const float4* twl,
                                               float* __restrict__ coh) {
   using P = FftPlan<LOGN>;
   using G = WctGeom<LOGN>;
-  constexpr int K0 = P::N >> (4 * Q + 1);
+  constexpr int K0 = BandGeom<LOGN, EC>::H;  // the window's half band: bins [-K0, K0)
   const int LO = K / 2;
   for (int r = r0; r < r1; r += G::ROWS) {
     const int jl = r + g;
@@ -1273,10 +1316,10 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
     // S1 S2 first (16 floats stay live, not 16 complex); |S12|^2 needs no phasor
     cpx v[16];
     float den[16];
-    smooth_from_band<LOGN, Q, TWL>(v, yz, slot, my, tw, t, par, twl);
+    smooth_from_band_ec<LOGN, EC, TWL>(v, yz, slot, my, tw, t, par, twl);
 #pragma unroll
     for (int m = 0; m < 16; ++m) den[m] = v[m].x * v[m].y;
-    smooth_from_band<LOGN, Q, TWL, false>(v, yw, slot, my, tw, t, par, twl);
+    smooth_from_band_ec<LOGN, EC, TWL, false>(v, yw, slot, my, tw, t, par, twl);
     if (valid) {
       const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
       put_row<LOGN, BUF, FULL>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
@@ -1429,21 +1472,24 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
   int par = 0;
   __syncthreads();
   const int nrow = j1 - j0;
-  auto key = [&](int r) {  // 1, 2: q windows; 4 + eu: wide windows; 0: not phase C's
+  auto key = [&](int r) {  // 16 + ec: q windows; 4 + eu: wide windows; 0: not phase C's
     const int pl = plan[j0 + r];
     if (!(pl & kPlanSpec)) return 0;
-    return plan_eu(pl) ? 4 + plan_eu(pl) : ((pl >> kPlanQwShift) & 3);
+    return plan_eu(pl) ? 4 + plan_eu(pl) : 16 + plan_ec(pl);
   };
   int r0 = 0;
   while (r0 < nrow) {
     const int q = key(r0);
     int r1 = r0 + 1;
     while (r1 < nrow && key(r1) == q) ++r1;
-    if constexpr (!WIDE && P::P16 >= 2 && (P::NT % 16) == 0 && (P::N >> 5) >= 16) {
-      if (q == 1) wct_spec_rows<LOGN, 1, BUF, TWL, FULL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
-      if constexpr (P::P16 >= 3 && (P::NT % 256) == 0 && (P::N >> 9) >= 16) {
-        if (q == 2) wct_spec_rows<LOGN, 2, BUF, TWL, FULL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
-      }
+    if constexpr (!WIDE) {
+#define WTMI_SC(EC)                                                                         \
+  if constexpr (spec_ec_ok<LOGN, EC>()) {                                                   \
+    if (q == 16 + EC)                                                                       \
+      wct_spec_rows<LOGN, EC, BUF, TWL, FULL>(a, SB, K, b, j0, r0, r1, my, tw, g, t, par, twl, coh); \
+  }
+      WTMI_SC(4) WTMI_SC(5) WTMI_SC(6) WTMI_SC(7) WTMI_SC(8) WTMI_SC(9)
+#undef WTMI_SC
     }
     if constexpr (WIDE && LOGN >= kWideMinLogn) {
       if (q == 5) wct_wide_rows<LOGN, 1, BUF, TWL, FULL>(a, WB, b, j0, r0, r1, my, tw, g, t, par, twl, coh);
@@ -1615,6 +1661,8 @@ static int launch_phase_a(CwtArgs& a, cpx* spec, cpx* TA, cpx* TB, cpx* SB, cpx*
     if (hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess) return launch_status();
     sa = side->s;
   }
+  // (the full-band rows in chunks of their own, 1 or 2 rows at 64 / 128 pairs, measured slower
+  // than the common 4: r04, profiles/r04/c4_shard_policy.txt)
   hipLaunchKernelGGL((wct_phase_a<LOGN, true, 0>), gd, dim3(G::BLOCK), 0, sa, a, spec, TA, TB, SB, DY, WB,
                      plan);
   if ((rc = launch_status()) != kOk) return rc;
