@@ -13,6 +13,7 @@ side streams do not leak across short-lived threads.
   with torch.cuda.graph and replayed; the replay equals direct launches bit for bit, also
   after the inputs change in place.
 * Side streams: a pool, not one per thread (include/wtmi.h wtmi_wct_side_streams).
+* Launch policies (r04): the scheduling options of the WCT give bitwise-identical outputs.
 """
 
 import threading
@@ -215,3 +216,38 @@ def test_side_streams_pooled_across_short_lived_threads():
         t.join()
     assert not errs, errs
     assert ops.wct_side_streams() == after
+
+
+@pytest.mark.parametrize("n0,B", [(1024, 6), (8192, 8), (16384, 3)])
+def test_wct_launch_policies_bitwise_equal(n0, B):
+    """The launch-policy options change only how the work is scheduled (r04): the decimation
+    classes in one launch or one per class (wct_dec_merge), the side stream and phase C's third
+    stream on or off, rows per workgroup -- every combination writes the same bits."""
+    from wtmi import _lib, ops, transforms
+    y1 = torch.tensor(red_batch(31, B, n0), device="cuda")
+    y2 = torch.tensor(red_batch(32, B, n0), device="cuda")
+    sj_h, _ = transforms.scales_for(n0, 1 / 12, 1 / 8, 2 / 12, -1, transforms.as_morlet(None))
+    sj = torch.tensor(sj_h, device="cuda")
+    K = transforms.boxcar_rows(transforms.as_morlet(None), 1 / 8)
+    ws = torch.empty(ops.wct_workspace_bytes(B, n0, sj_h.size), dtype=torch.uint8, device="cuda")
+
+    def run():
+        r = ops.wct_morlet(y1, y2, sj, 1 / 12, boxcar=K, want_uv=False, want_power=True,
+                           want_phase=True, workspace=ws, normalize=True)
+        torch.cuda.synchronize()
+        return {k: r[k].clone() for k in ("coh", "power", "phase")}
+
+    ref = run()
+    for opts in ({"wct_dec_merge": 0}, {"wct_dec_merge": 1}, {"wct_side_stream": 0},
+                 {"wct_pc_early": 0}, {"wct_pc_early": 1}, {"wct_min_rows": 1},
+                 {"wct_dec_merge": 1, "wct_min_rows": 2, "wct_dec_rows": 2}):
+        ctx = [_lib.option(k, v) for k, v in opts.items()]
+        for c in ctx:
+            c.__enter__()
+        try:
+            out = run()
+        finally:
+            for c in reversed(ctx):
+                c.__exit__(None, None, None)
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), (opts, k)
