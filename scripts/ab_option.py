@@ -1,8 +1,9 @@
 """A/B of a launch option on one config's step, alternating in one process (rounds x values),
 results checked bitwise equal across values:
 
-    python scripts/ab_option.py c3a|c3s|c4 OPTION V0 V1 [V2 ...] [--reps R]
-c3a: C3's analysis (8192 x 16384, J = 10); c3s: its synthesis; c4: the C4 step (512 pairs)."""
+    python scripts/ab_option.py c2|c3a|c3s|c4 OPTION V0 V1 [V2 ...] [--reps R]
+c2: the C2 step (1024 series, or --batch); c3a: C3's analysis (8192 x 16384, J = 10); c3s: its
+synthesis; c4: the C4 step (512 pairs)."""
 import argparse
 import sys
 
@@ -21,7 +22,16 @@ ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--batch", type=int, default=512, help="c4: pairs")
 a = ap.parse_args()
-if a.what in ("c3a", "c3s"):
+if a.what == "c2":
+    DT = 1 / 12
+    sj = torch.tensor(2 * DT * 2 ** (np.arange(128) / 12), device="cuda")
+    x = torch.randn(a.batch if a.batch != 512 else 1024, 4096, device="cuda")
+    out = torch.empty((x.shape[0], 128, 4096), dtype=torch.complex64, device="cuda")
+
+    def step():
+        ops.cwt_morlet(x, sj, DT, 6.0, out_w=out)
+        return out
+elif a.what in ("c3a", "c3s"):
     w = Wavelet("db4")
     B, n, J = 8192, 16384, 10
     x = torch.randn(B, n, device="cuda")
