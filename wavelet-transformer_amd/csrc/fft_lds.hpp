@@ -274,6 +274,32 @@ __device__ __forceinline__ void xl_swap(cpx& x, cpx& y) {
   y = mkc(yr, yi);
 }
 
+// Four xl_swap at once (q = 4h .. 4h + 3): 8 swaps between one pair of wait-state blocks instead
+// of four pairs (the swaps touch disjoint VGPRs, so none waits on another).
+__device__ __forceinline__ void xl_swap4(cpx* v) {
+  float r[8], i[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    r[k] = v[k].x;
+    i[k] = v[k].y;
+  }
+  asm volatile(
+      "s_nop 4\n\t"
+      "v_permlane32_swap_b32 %0, %1\n\t"
+      "v_permlane32_swap_b32 %2, %3\n\t"
+      "v_permlane32_swap_b32 %4, %5\n\t"
+      "v_permlane32_swap_b32 %6, %7\n\t"
+      "v_permlane32_swap_b32 %8, %9\n\t"
+      "v_permlane32_swap_b32 %10, %11\n\t"
+      "v_permlane32_swap_b32 %12, %13\n\t"
+      "v_permlane32_swap_b32 %14, %15\n\t"
+      "s_nop 1"
+      : "+v"(r[0]), "+v"(r[1]), "+v"(i[0]), "+v"(i[1]), "+v"(r[2]), "+v"(r[3]), "+v"(i[2]), "+v"(i[3]),
+        "+v"(r[4]), "+v"(r[5]), "+v"(i[4]), "+v"(i[5]), "+v"(r[6]), "+v"(r[7]), "+v"(i[6]), "+v"(i[7]));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = mkc(r[k], i[k]);
+}
+
 // Offset of pass p's entries in the LDS twiddle table.
 __host__ __device__ constexpr int twl_base(int p) { return p <= 1 ? 0 : 16; }
 
@@ -583,8 +609,9 @@ __device__ __forceinline__ void fft_row(cpx (&v)[16], cpx* __restrict__ lds, int
       constexpr int tb = TWL ? 0 : 4 * (P::P16 - 1);
       if constexpr (P::XL && NBUF == 1) {
         static_assert(R == 2, "XL rows end with a radix-2 pass");
-#pragma unroll
-        for (int q = 0; q < Q; ++q) xl_swap(v[2 * q], v[2 * q + 1]);
+        static_assert(Q == 8, "XL tail: 8 radix-2 butterflies per thread");
+        xl_swap4(v);
+        xl_swap4(v + 8);
       } else {
 #pragma unroll
         for (int q = 0; q < Q; ++q)
