@@ -255,27 +255,15 @@ __device__ __forceinline__ int fft_thread(int rt) {
 // (t / 256) 4096 + t mod 256 + 256 r; the radix-2 tail of thread t needs positions
 // t + 512 q and t + 512 q + 4096.  With X = v[2q], Y = v[2q+1], swapping the upper half of X
 // with the lower half of Y leaves (X, Y) = (x[t + 512 q], x[t + 512 q + 4096]) in every lane.
-// Both swaps sit in ONE asm block: the compiler's hazard recognizer cannot see into inline
-// asm, so nothing it schedules may land between them, and the block carries its own wait
-// states -- 5 ahead (gfx950 needs 2 after a VALU write of a swapped VGPR, 4 after a v_cmpx
-// exec write) and 2 behind (a VALU read of a swap result).  gfx950 only.
+// The swaps of four such pairs (q = 4h .. 4h + 3: 8 v_permlane32_swap on disjoint VGPRs, so none
+// waits on another; r04, two blocks per tail instead of eight) sit in ONE asm block: the
+// compiler's hazard recognizer cannot see into inline asm, so nothing it schedules may land
+// between them, and the block carries its own wait states -- 5 ahead (gfx950 needs 2 after a
+// VALU write of a swapped VGPR, 4 after a v_cmpx exec write) and 2 behind (a VALU read of a swap
+// result).  gfx950 only.
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "wtmi kernels are written for gfx950 (v_permlane32_swap)"
 #endif
-__device__ __forceinline__ void xl_swap(cpx& x, cpx& y) {
-  float xr = x.x, xi = x.y, yr = y.x, yi = y.y;
-  asm volatile(
-      "s_nop 4\n\t"
-      "v_permlane32_swap_b32 %0, %1\n\t"
-      "v_permlane32_swap_b32 %2, %3\n\t"
-      "s_nop 1"
-      : "+v"(xr), "+v"(yr), "+v"(xi), "+v"(yi));
-  x = mkc(xr, xi);
-  y = mkc(yr, yi);
-}
-
-// Four xl_swap at once (q = 4h .. 4h + 3): 8 swaps between one pair of wait-state blocks instead
-// of four pairs (the swaps touch disjoint VGPRs, so none waits on another).
 __device__ __forceinline__ void xl_swap4(cpx* v) {
   float r[8], i[8];
 #pragma unroll
