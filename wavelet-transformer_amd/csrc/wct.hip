@@ -1510,11 +1510,12 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
 // r04 re-sweep after the merged decimation launch and phase C's third stream (one box,
 // alternating in one process, ms for min rows 1 / 2 / 3 / 4): 64 pairs 0.458 / 0.450 / 0.449 /
 // 0.449, 128 pairs 0.870 / 0.826 / 0.818 / 0.802, 256 pairs 1.656 / 1.635 / 1.637 / 1.562, 512
-// pairs 3.235 / 3.132 / 3.106 / 3.073: four rows per workgroup at every batch.
+// pairs 3.235 / 3.132 / 3.106 / 3.073: four rows per workgroup from 64 pairs on.  A handful of
+// pairs (the app's single-pair calls) keeps one row per workgroup: there the grid is a few
+// dozen workgroups and the step is as long as one workgroup's rows.
 static int wct_min_rows(long long batch) {
-  (void)batch;
   const int o = options().wct_min_rows;
-  return o > 0 ? o : 4;
+  return o > 0 ? o : (batch <= 32 ? 1 : 4);
 }
 static int wct_dec_rows_per_wg(long long batch) {
   const int o = options().wct_dec_rows;
