@@ -223,6 +223,7 @@ class C2(Workload):
     name, axis, seed = "c2", "series", 1002
     B, n0, dj, J = 1024, 4096, 1 / 12, 127
     kernel = "cwt_morlet_kernel<12,1,0,0>"
+    PER_STEP = {"wtmi::cwt_morlet_kernel<12": 1}  # kernel-name prefix -> launches per step
 
     def setup(self):
         torch = self.torch
@@ -233,7 +234,7 @@ class C2(Workload):
                                device=self.dev)
         self.units = self.local * self.sj.size * self.n0
         self.bytes = self.units * 8 + self.local * self.n0 * 4  # W write + x read
-        self.per_step = {"wtmi::" + self.kernel.split(",")[0]: 1}
+        self.per_step = dict(self.PER_STEP)
         self.bytes_note = "8 B/coeff complex64 W write + 4 B/sample x read"
 
     def step(self):
@@ -308,6 +309,7 @@ class C3(Workload):
     name, axis, seed = "c3", "series", 1003
     B, n, J = 8192, 16384, 10
     kernel = "modwt_vec_kernel<8,4,1024,16>+imodwt_hyb_kernel<8,8,512,2,4>"
+    PER_STEP = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_hyb_kernel<": 1}
 
     def setup(self):
         from wtmi.wavelets import Wavelet
@@ -318,7 +320,7 @@ class C3(Workload):
         self.x = self.torch.tensor(x, device=self.dev)
         self.units = self.local * (self.J + 1) * self.n
         self.bytes = self.local * self.n * 96  # 4 x + 44 W write + 44 W read + 4 x^
-        self.per_step = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_hyb_kernel<": 1}
+        self.per_step = dict(self.PER_STEP)
         self.bytes_note = "96 B per series-sample (x, W write, W read, x^)"
 
     def step(self):
@@ -343,6 +345,9 @@ class C4(Workload):
               "wct_phase_a<13,decimated rows> + wct_phase_b<10> [caller's stream], "
               "wct_wide_boxcar<10> + wct_phase_c<13,q windows> + wct_phase_c<13,wide windows> "
               "[side stream]; joined on the caller's stream")
+    # every wtmi::wct_* kernel of the step once (r03: the normalisation runs inside
+    # wct_spectra_plan; no separate moments launches)
+    PER_STEP = {"wtmi::wct_": 1}
 
     def setup(self):
         from wtmi import transforms
@@ -359,9 +364,7 @@ class C4(Workload):
         self.bytes = self.units * 12 + self.local * self.n * 8
         self.ws = torch.empty(self.ops.wct_workspace_bytes(max(self.local, 1), self.n, S),
                               dtype=torch.uint8, device=dev)
-        # every wtmi::wct_* kernel of the step once (r03: the normalisation runs inside
-        # wct_spectra_plan; no separate moments launches)
-        self.per_step = {"wtmi::wct_": 1}
+        self.per_step = dict(self.PER_STEP)
         self.bytes_note = "12 B/coeff (|W12|^2 + WCT + phase, f32) + 8 B/pair-sample inputs"
 
     def step(self):
@@ -450,6 +453,41 @@ def kernel_roofline(cfg):
             keep = ("kernel", "ms", "bound", "frac", "hbm_GBps", "hbm_frac", "valu_busy")
             return [{k: r[k] for k in keep} for r in ent["kernels"]], os.path.relpath(path, ROOT)
     return None, None
+
+
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 4  # 1024 SIMDs x 2.4 GHz, one wave64 VALU op per 4 cycles
+
+
+def step_bound(cfg, per_step, step_ms, hbm_frac):
+    """The step's binding resource from the newest committed per-kernel profile: the HBM
+    fraction of the step (algorithmic bytes / step time / peak, measured live) beside its VALU
+    fraction (the profile's SQ_INSTS_VALU of every kernel of the step x 4 cycles, over the
+    chip's 1024 SIMDs x 2.4 GHz x the live step time); bound = the larger.  Without a profile
+    holding every kernel of the step: "hbm" and no VALU fraction."""
+    import glob
+    out = {"bound": "hbm", "hbm": hbm_frac, "valu": None, "valu_insts_per_step": None,
+           "source": None}
+    if not per_step or not step_ms:
+        return out
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_roofline.json")), reverse=True):
+        with open(path) as fh:
+            ent = json.load(fh).get(cfg)
+        if not ent:
+            continue
+        insts, seen = 0.0, 0
+        for prefix, count in per_step.items():
+            hits = [k for k in ent["kernels"] if k["kernel"].startswith(prefix) and k.get("valu_insts")]
+            if not hits:
+                break
+            insts += sum(k["valu_insts"] for k in hits) * count
+            seen += 1
+        if seen != len(per_step):
+            continue
+        valu = insts / (VALU_PEAK_WAVE_INSTS * step_ms * 1e-3)
+        out.update(bound="valu" if valu > hbm_frac else "hbm", valu=valu, valu_insts_per_step=insts,
+                   source=os.path.relpath(path, ROOT))
+        return out
+    return out
 
 
 def pmc_traffic(cfg, per_step):
@@ -571,6 +609,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one GPU per rank: the measured mode) or gloo (smoke mode: "
                          "ranks may share a GPU, rank r on cuda:(r mod device count))")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group even at --gpus 1 (RANK 0 of WORLD_SIZE 1 on "
+                         "127.0.0.1): the RCCL barrier / all-reduce / gloo side-group gather run on "
+                         "one GPU")
     ap.add_argument("--rank-timeout", type=float, default=0.0,
                     help="self-launched ranks: wall-clock limit in seconds (0 = none)")
     args = ap.parse_args()
@@ -614,7 +656,17 @@ def main():
     else:
         dev = torch.device("cpu")
         sync = lambda: None  # noqa: E731
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
+        if world == 1:  # --force-dist without a launcher: a one-rank group on 127.0.0.1
+            import socket
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                with socket.socket() as s:
+                    s.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if rccl:
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -624,7 +676,7 @@ def main():
     sync()
 
     def barrier():
-        if world > 1:
+        if dist_on:
             if rccl:
                 dist.barrier(device_ids=[dev.index])
             else:
@@ -697,6 +749,13 @@ def main():
     own_max, own_min = sharding.max_over_ranks(t_own), -sharding.max_over_ranks(-t_own)
     bar_max, bar_min = sharding.max_over_ranks(t_barrier), -sharding.max_over_ranks(-t_barrier)
     check = wl.check() if rank == 0 and wl.local else None
+    gathered = None
+    if dist_on:
+        # the host-side gather of sharding.gather_to_rank0 (a gloo side group under RCCL):
+        # every rank's first row count and units, gathered on rank 0
+        mine = torch.tensor([[float(wl.lo), float(wl.units)]], dtype=torch.float64)
+        g = sharding.gather_to_rank0(mine, world)
+        gathered = None if g is None else g.tolist()
     if want_cpu and cpu is None:  # after the timed region (default)
         cpu = cpu_baseline_child(args)
 
@@ -704,10 +763,12 @@ def main():
         achieved = wl.bytes / (kern_ms * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(args.config, wl.per_step)
         per_kernel, ksrc = kernel_roofline(args.config)
+        sb = step_bound(args.config, wl.per_step, kern_ms, achieved / HBM_PEAK_GBS)
         cfg = wl.config()
         cfg.update(wl.shard_config(world, args.scaling))
-        if world > 1:
+        if dist_on:
             cfg["dist_backend"] = "rccl" if rccl else "gloo"
+            cfg["dist_gather"] = gathered
             if not rccl and args.device == "cuda":
                 cfg["devices"] = "shared: rank r on cuda:(r mod %d) (gloo smoke mode, not a scaling "\
                                  "measurement)" % torch.cuda.device_count()
@@ -727,8 +788,15 @@ def main():
             "data": "synthetic: seeded AR(1) red noise (a=0.7) + 3 random sinusoids per series, "
                     "resident in HBM before timing",
             "config": cfg,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": sb["bound"], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "step_fractions": {"hbm": sb["hbm"], "valu": sb["valu"],
+                                            "valu_insts_per_step": sb["valu_insts_per_step"],
+                                            "valu_peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 "
+                                                         "VALU instruction",
+                                            "source": sb["source"],
+                                            "note": "achieved / peak / frac above are the HBM "
+                                                    "fraction; bound is the larger of the two"},
                          "traffic_source": tsrc, "scope": "rank 0's launches",
                          "kernel": wl.kernel, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": wl.bytes, "bytes_model": wl.bytes_note,
@@ -743,7 +811,7 @@ def main():
             "graph": bool(use_graph),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     return 0
 

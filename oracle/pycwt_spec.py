@@ -338,7 +338,7 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
         a2, _, _ = ar1(y2)
         sig = wct_significance(a1, a2, dt=dt, dj=dj, s0=s0, J=J,
                                significance_level=significance_level, wavelet=wavelet,
-                               **{k: v for k, v in kwargs.items() if k in ("mc_count", "rng", "noise")})
+                               **{k: v for k, v in kwargs.items() if k in ("mc_count", "rng", "noise", "quantile")})
     else:
         sig = np.asarray([0])
     return WCT, aWCT, coi, freq, sig
@@ -408,14 +408,47 @@ def coherence_histogram(R2, outsidecoi, maxscale, nbins=1000, wlc=None):
     return wlc
 
 
-def significance_from_histogram(wlc, outsidecoi, maxscale, significance_level=0.95):
-    """sig95 from the per-scale counters: NaN for scales with points outside the COI,
-    then for s < maxscale the significance_level quantile interpolated on the
-    mid-bin coherence grid over the non-empty bins (P = (cumsum - 0.5) / total)."""
+PYCWT_QUANTILE_ERROR = "object too deep for desired array"
+
+
+def significance_from_histogram(wlc, outsidecoi, maxscale, significance_level=0.95,
+                                quantile="pycwt"):
+    """sig95 from the per-scale counters: NaN for scales with points outside the COI, then
+    the quantile step for s < maxscale.
+
+    quantile="pycwt" executes pycwt 0.4.0b0's published statements literally (DESIGN 4,
+    "Monte-Carlo quantile"):
+
+        wlc = np.ma.zeros([J + 1, nbins])          # never masked: mask is np.ma.nomask
+        ...                                        # wlc[s, int(t)] += 1 per outside-COI point
+        R2y = (np.arange(nbins) + 0.5) / nbins
+        for s in range(maxscale):
+            sel = ~wlc[s, :].mask                  # ~nomask: the scalar np.True_
+            P = wlc[s, sel].data.cumsum()          # a 0-d boolean index adds an axis: (1, nbins)
+            P = (P - 0.5) / P[-1]
+            sig95[s] = np.interp(significance_level, P, R2y[sel])   # R2y[sel]: (1, nbins)
+
+    np.interp needs a 1-D fp, so it raises ValueError("object too deep for desired array")
+    under numpy 1.26.4 (the reference's pin, requirements.txt:25) and 2.x alike
+    (tests/test_wct_sig_host.py runs these lines in both).  quantile="nonempty" is the
+    engine's explicit alternative: interpolation over each scale's non-empty bins (what a
+    masked counter would have selected)."""
+    if quantile not in ("pycwt", "nonempty"):
+        raise ValueError(quantile)
     nbins = wlc.shape[1]
     sig95 = np.zeros(wlc.shape[0])
     sig95[outsidecoi.any(axis=1)] = np.nan
     R2y = (np.arange(nbins) + 0.5) / nbins
+    if quantile == "pycwt":
+        counter = np.ma.zeros(wlc.shape)
+        counter[:, :] = wlc
+        with np.errstate(invalid="ignore", divide="ignore"):
+            for s in range(maxscale):
+                sel = ~counter[s, :].mask
+                P = counter[s, sel].data.cumsum()
+                P = (P - 0.5) / P[-1]
+                sig95[s] = np.interp(significance_level, P, R2y[sel])
+        return sig95
     for s in range(maxscale):
         sel = wlc[s, :] != 0
         P = wlc[s, sel].cumsum()
@@ -424,10 +457,28 @@ def significance_from_histogram(wlc, outsidecoi, maxscale, significance_level=0.
     return sig95
 
 
+def pycwt_cache_name(al1, al2, dt, dj, s0, J, wavelet_name="morlet"):
+    """pycwt 0.4.0b0 ``wct_significance``'s cache file name, as published:
+
+        aa = np.round(np.arctanh(np.array([al1, al2]) * 4))
+        aa = np.abs(aa) + 0.5 * (aa < 0)
+        cache = 'wct_sig_{:0.5f}_{:0.5f}_{:0.5f}_{:0.5f}_{:d}_{}'.format(
+            aa[0], aa[1], dj, s0 / dt, J, wavelet.name)
+
+    arctanh(4 al) is NaN for |al| > 0.25, so every such series shares the name's 'nan'
+    fields (the engine keys on the exact al instead)."""
+    with np.errstate(invalid="ignore", divide="ignore"):
+        aa = np.round(np.arctanh(np.array([al1, al2]) * 4))
+    aa = np.abs(aa) + 0.5 * (aa < 0)
+    return "wct_sig_{:0.5f}_{:0.5f}_{:0.5f}_{:0.5f}_{:d}_{}".format(
+        aa[0], aa[1], dj, s0 / dt, J, wavelet_name)
+
+
 def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet=None,
-                     mc_count=300, rng=None, nbins=1000, noise="pycwt"):
+                     mc_count=300, rng=None, nbins=1000, noise="pycwt", quantile="pycwt"):
     """pycwt ``wct_significance`` without the disk cache; ``noise`` as in
-    ``rednoise``."""
+    ``rednoise``, ``quantile`` as in ``significance_from_histogram`` (the literal "pycwt"
+    reading raises ValueError after the Monte Carlo whenever maxscale > 0)."""
     wavelet = wavelet or Morlet(6)
     rng = rng if rng is not None else np.random.default_rng()
     N, sj, outsidecoi, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
@@ -445,4 +496,4 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet=N
         S12 = wavelet.smooth(nW12 / scales, dt, dj, sj)
         R2 = np.abs(S12) ** 2 / (S1 * S2)
         coherence_histogram(R2, outsidecoi, maxscale, nbins, wlc)
-    return significance_from_histogram(wlc, outsidecoi, maxscale, significance_level)
+    return significance_from_histogram(wlc, outsidecoi, maxscale, significance_level, quantile)

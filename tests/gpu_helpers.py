@@ -1,6 +1,28 @@
 """Shared helpers for the @gpu parity tests."""
 
+import json
+import os
+
 import numpy as np
+
+# CWT / XWT per (series, scale) row ||W - W_ref|| / ||W_ref|| <= 1e-5, "the same
+# applies to power" (and to W12, the XWT power and the significance ratio).
+ROW_TOL = 1e-5
+
+
+def gate(name, err, tol=ROW_TOL):
+    """Assert max(err) <= tol and print the measured maximum.  With WTMI_PARITY_LOG set, the
+    (test, check, max, gate) record is appended there as one JSON line (DESIGN.md section 4's
+    table of measured maxima is built from that file)."""
+    worst = float(np.max(err)) if np.size(err) else 0.0
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    print(f"PARITY {test} {name}: max {worst:.3e} (gate {tol:.0e})")
+    log = os.environ.get("WTMI_PARITY_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"test": test, "check": name, "max": worst, "gate": tol}) + "\n")
+    assert worst <= tol, (name, worst, tol)
+    return worst
 
 
 def red_series(rng, n, a=0.7, dtype=np.float32):

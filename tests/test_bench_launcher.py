@@ -116,3 +116,36 @@ def test_per_rank_timing_fields():
     assert 0 <= rk["closing_barrier_ms"]["min"] <= rk["closing_barrier_ms"]["max"]
     assert rk["own_steps_ms_per_step"]["max"] <= d["ms_per_step"] * 1.0001
     assert d["graph"] is False
+
+
+def test_force_dist_runs_a_one_rank_group_with_the_gather():
+    """--force-dist at --gpus 1 initialises the process group (here gloo on CPU; on the GPU box
+    RCCL, tests/test_gpu_dist.py) and runs the barrier, the max / sum over ranks and the
+    host-side gather of sharding.gather_to_rank0."""
+    r, d = _run("--gpus", "1", "--force-dist", "--dist-backend", "gloo")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert d["config"]["dist_backend"] == "gloo"
+    assert d["config"]["dist_gather"] == [[0.0, 10 * 256.0]]
+    r, d = _run("--gpus", "2", "--dist-backend", "gloo")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert d["config"]["dist_gather"] == [[0.0, 10 * 256.0], [10.0, 10 * 256.0]]
+
+
+@pytest.mark.parametrize("cfg,bound", [("c2", "hbm"), ("c3", "hbm"), ("c4", "valu")])
+def test_roofline_bound_follows_the_committed_profile(cfg, bound):
+    """roofline.bound is the larger of the step's HBM fraction and its VALU fraction (the
+    newest committed kernel_roofline.json's SQ_INSTS_VALU of the step's kernels over the
+    chip's VALU issue rate): C4's kernels are VALU-bound, C2 / C3 sit on HBM.  Checked at the
+    step times and HBM fractions of the committed bench lines."""
+    import glob
+    sys.path.insert(0, ROOT)
+    import bench
+    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"bench_{cfg}.json")))[-1]
+    with open(prof) as fh:
+        line = json.load(fh)
+    hbm = line["roofline"]["achieved"] / line["roofline"]["peak"]
+    sb = bench.step_bound(cfg, bench.CONFIGS[cfg].PER_STEP, line["roofline"]["kernel_ms"], hbm)
+    assert sb["bound"] == bound, sb
+    assert sb["source"] and 0 < sb["valu"] < 1 and sb["hbm"] == hbm
+    if "step_fractions" in line["roofline"]:  # lines written since the field exists
+        assert line["roofline"]["bound"] == bound

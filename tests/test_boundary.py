@@ -177,6 +177,21 @@ def test_run_cwt_unknown_kwarg_raises_typeerror(modules):
         transforms.standardize_coefs(None, detrendd=True)
 
 
+def test_create_xwt_results_dict_fails_only_at_a_pair(modules):
+    """The reference loops over xwt_list calling run_xwt(data, **kwargs)
+    (src/utils/transform_helpers.py:126-135): no pairs -> {} whatever the keywords; the first
+    pair is looked up (KeyError) before run_xwt's TypeError / NameError."""
+    from src.utils import transform_helpers as th
+    assert th.create_xwt_results_dict({}, [], normalize=False) == {}
+    assert th.create_xwt_results_dict({}, [], bogus=1) == {}
+    with pytest.raises(KeyError):
+        th.create_xwt_results_dict({}, [("a", "b")], normalize=False)
+    with pytest.raises(NameError):
+        th.create_xwt_results_dict({("a", "b"): None}, [("a", "b")], normalize=False)
+    with pytest.raises(TypeError):
+        th.create_xwt_results_dict({("a", "b"): None}, [("a", "b")], bogus=1)
+
+
 # ------------------------------------------------------------------------ overlay
 FAKE_REF = {
     "src/__init__.py": "",

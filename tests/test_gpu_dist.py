@@ -105,3 +105,63 @@ def test_bench_two_ranks_gloo_smoke(scaling, glob, per):
     assert cfg["dist_backend"] == "gloo"
     assert line["value"] > 0
     assert line["check"]["rank0_first_last_series_max_row_rel_err_vs_oracle"] < 1e-5
+
+
+def _rccl_main(port, out_dir):
+    """One rank of an RCCL group of one on cuda:0: the barrier with device_ids, the max / sum
+    over ranks on device tensors, and the host-side gather through the gloo side group that
+    sharding.host_group creates under RCCL (bench.py's and sharding's RCCL branch)."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "wavelet-transformer_amd"), os.path.join(ROOT, "tests")]
+    import torch
+    import torch.distributed as dist
+    from wtmi import sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    assert dist.get_backend() == "nccl"
+    dist.barrier(device_ids=[0])
+    W, M = _transform(_batch())
+    gW = sharding.gather_to_rank0(torch.view_as_real(W), B)
+    gM = sharding.gather_to_rank0(M, B)
+    assert str(dist.get_backend(sharding.host_group())) == "gloo"
+    t = sharding.max_over_ranks(2.5)
+    u = sharding.sum_over_ranks(7.0)
+    np.save(os.path.join(out_dir, "W.npy"), torch.view_as_complex(gW).numpy())
+    np.save(os.path.join(out_dir, "M.npy"), gM.numpy())
+    np.save(os.path.join(out_dir, "tu.npy"), np.array([t, u]))
+    dist.barrier(device_ids=[0])
+    dist.destroy_process_group()
+
+
+def test_rccl_branch_one_rank(tmp_path):
+    """the RCCL code path on the one-GPU box (a fresh child process): init with
+    device_id, barrier(device_ids=[0]), all-reduces on device tensors, the gloo side group of
+    the gather; the gathered batch is bit-identical to a direct transform."""
+    port = _free_port()
+    code = ("import sys; sys.path[:0] = [%r, %r]; import test_gpu_dist as t; t._rccl_main(%d, %r)"
+            % (os.path.join(ROOT, "tests"), ROOT, port, str(tmp_path)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    W, M = _transform(_batch())
+    np.testing.assert_array_equal(np.load(tmp_path / "W.npy"), W.cpu().numpy())
+    np.testing.assert_array_equal(np.load(tmp_path / "M.npy"), M.cpu().numpy())
+    np.testing.assert_array_equal(np.load(tmp_path / "tu.npy"), [2.5, 7.0])
+
+
+def test_bench_force_dist_rccl():
+    """bench.py --force-dist at --gpus 1: the measured path's RCCL group (one rank), its timing
+    barrier and reductions, and the host gather; the JSON line says dist_backend "rccl"."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "c2",
+           "--force-dist", "--steps", "3", "--warmup", "1", "--prewarm-s", "0",
+           "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["config"]["dist_backend"] == "rccl"
+    assert line["config"]["dist_gather"] == [[0.0, 1024 * 128 * 4096.0]]
+    assert line["value"] > 0
+    assert line["check"]["rank0_first_last_series_max_row_rel_err_vs_oracle"] < 1e-5

@@ -6,14 +6,14 @@ the WCT over 512 pairs, C2's 4.3 GB W and C3's 5.9 GB decomposition (the last se
 at the highest addresses), and a full C5 streaming chunk.  Rows are sampled at the start,
 middle and END of each batch.  Tolerances as SURVEY 8(d): CWT row-normwise <= 1e-5, MODWT
 per-row normwise <= 1e-5 and round trip <= 1e-5 max|x|, WCT coherence abs <= 1e-4,
-power row-normwise <= 5e-5, phase <= 1e-4 rad where |W12| > 1e-3 max.
+power row-normwise <= 1e-5, phase <= 1e-4 rad where |W12| > 1e-3 max.
 """
 
 import numpy as np
 import pytest
 import torch
 
-from gpu_helpers import red_batch, row_relerr
+from gpu_helpers import gate, red_batch, row_relerr
 from oracle import modwt_spec as ms
 from oracle import pycwt_spec as pc
 
@@ -25,8 +25,7 @@ def _cwt_rows_ok(W, x, rows, dj, J):
     for r in rows:
         ref = pc.cwt(x[r].astype(np.float64), DT, dj, 2 * DT, J)[0]
         got = W[r].cpu().numpy().astype(np.complex128)
-        err = row_relerr(got, ref).max()
-        assert err <= 1e-5, (r, err)
+        gate(f"W[{r}]", row_relerr(got, ref))
 
 
 def test_c2_full_batch():
@@ -64,7 +63,7 @@ def test_cwt_full_size_linearity_every_series(B, n, dj, J):
              + 2 * torch.linalg.vector_norm(wy[c:c + 128], dim=-1))
         assert bool((s > 0).all())
         worst = max(worst, (d / s).max().item())
-    assert worst <= 1e-5, worst
+    gate("linearity every row", worst)
     del wx, wy, wz
     torch.cuda.empty_cache()
 
@@ -129,14 +128,14 @@ def test_c4_full_batch():
     for p in (0, 255, 511):
         a1, a2 = y1[p].astype(np.float64), y2[p].astype(np.float64)
         rc = pc.wct(a1, a2, DT, dj=dj, s0=2 * DT, J=-1, sig=False)[0]
-        assert np.abs(res["coh"][p].cpu().numpy() - rc).max() <= 1e-4, p
+        gate(f"coherence abs[{p}]", np.abs(res["coh"][p].cpu().numpy() - rc), 1e-4)
         W12 = (pc.cwt((a1 - a1.mean()) / a1.std(), DT, dj, 2 * DT, -1)[0]
                * pc.cwt((a2 - a2.mean()) / a2.std(), DT, dj, 2 * DT, -1)[0].conj())
         pw = res["power"][p].cpu().numpy().astype(np.float64)
-        assert row_relerr(pw, np.abs(W12) ** 2).max() <= 5e-5, p
+        gate(f"wct power[{p}]", row_relerr(pw, np.abs(W12) ** 2))
         mask = np.abs(W12) > 1e-3 * np.abs(W12).max()
         dphi = np.angle(np.exp(1j * (res["phase"][p].cpu().numpy() - np.angle(W12))))
-        assert np.abs(dphi[mask]).max() <= 1e-4, p
+        gate(f"phase rad[{p}]", np.abs(dphi[mask]), 1e-4)
     del res
     torch.cuda.empty_cache()
 

@@ -1,7 +1,7 @@
 """Series longer than one workgroup's row (n0 > 16384 -> the four-step long-row path,
 csrc/fft_long.hpp) and boxcar windows wider than the register ring (K > 24), vs the
 oracle (pycwt restatement).  Tolerances as SURVEY 8(d): CWT / XWT rows <= 1e-5
-row-normwise (XWT power 5e-5), coherence abs <= 1e-4, phase <= 1e-4 rad where
+row-normwise (power, W12 too), coherence abs <= 1e-4, phase <= 1e-4 rad where
 |W12| > 1e-3 max.  The reference (pycwt over scipy.fftpack) has no length limit; the
 engine transforms up to 2^20 samples per row.
 """
@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_helpers import red_batch, row_relerr
+from gpu_helpers import gate, red_batch, row_relerr
 from oracle import pycwt_spec as pc
 
 pytestmark = pytest.mark.gpu
@@ -33,8 +33,8 @@ def test_long_cwt_matches_oracle(n0, dj, J):
     for b in range(2):
         ref = pc.cwt(x[b].astype(np.float64), DT, dj, 2 * DT, J)[0]
         assert W.shape[1:] == ref.shape
-        assert row_relerr(W[b].astype(np.complex128), ref).max() <= 1e-5, b
-        assert row_relerr(P[b].astype(np.float64), np.abs(ref) ** 2).max() <= 2e-5, b
+        gate(f"W[{b}]", row_relerr(W[b].astype(np.complex128), ref))
+        gate(f"power[{b}]", row_relerr(P[b].astype(np.float64), np.abs(ref) ** 2))
 
 
 def test_long_cwt_per_series_significance_and_chunking():
@@ -51,7 +51,7 @@ def test_long_cwt_per_series_significance_and_chunking():
     for b in range(B):
         np.testing.assert_allclose(s[b], p[b] * (1.0 + b), rtol=1e-6)
     ref = np.abs(pc.cwt(x[2].astype(np.float64), DT, dj, 2 * DT, J)[0]) ** 2
-    assert row_relerr(p[2].astype(np.float64), ref).max() <= 2e-5
+    gate("power[2]", row_relerr(p[2].astype(np.float64), ref))
 
 
 def test_long_xwt_pair_outputs():
@@ -66,7 +66,8 @@ def test_long_xwt_pair_outputs():
         W12 = (pc.cwt(y1[b].astype(np.float64), DT, dj, 2 * DT, J)[0]
                * pc.cwt(y2[b].astype(np.float64), DT, dj, 2 * DT, J)[0].conj())
         got = r["w12"][b].cpu().numpy().astype(np.complex128)
-        assert row_relerr(got, W12).max() <= 5e-5
+        gate(f"W12[{b}]", row_relerr(got, W12))
+        gate(f"xwt power[{b}]", row_relerr(r["power"][b].cpu().numpy().astype(np.float64), np.abs(W12) ** 2))
         mask = np.abs(W12) > 1e-3 * np.abs(W12).max()
         ang = np.angle(W12)
         np.testing.assert_allclose(r["u"][b].cpu().numpy()[mask], np.sin(ang[mask]), atol=1e-4)
@@ -111,7 +112,8 @@ def test_wct_significance_long_noise():
     J = int(np.round(np.log2(n0 * DT / s0) / dj))
     N, sj, _, _, anyout, maxscale = transforms.wct_sig_geometry(DT, dj, s0, J)
     assert N > 16384
-    sig = transforms.wct_significance(0.6, 0.4, DT, dj, s0, J, mc_count=60, cache=False, seed=3)
+    sig = transforms.wct_significance(0.6, 0.4, DT, dj, s0, J, mc_count=60, cache=False, seed=3,
+                                      quantile="nonempty")
     assert sig.shape == (J + 1,)
     ok = sig[:maxscale]
     assert np.isfinite(ok).all() and (ok > 0).all() and (ok <= 1).all()

@@ -873,7 +873,7 @@ __global__ void __launch_bounds__((WctGeom<LOGN>::BLOCK), (WctGeom<LOGN>::MINW))
     const int q = q_tab[r0];
     int r1 = r0 + 1;
     while (r1 < nrow && q_tab[r1] == q) ++r1;
-    if (q >= 4) {  // decimated rows (full rows only)    } else if (q >= 4) {  // decimated rows (full rows only)
+    if (q >= 4) {  // decimated rows (full rows only)
       if constexpr (KIND == 2 && FULL && LOGN >= kDecMinLogn) {
         switch (q - 4) {
 #define WTMI_DR(EE)                                                                     \
@@ -1526,17 +1526,18 @@ static int wct_dec_rows_per_wg(long long batch) {
 // Side streams for the full-band rows' kernel beside the decimated rows' chain (fork after the
 // plan, join before the caller's stream proceeds).  A small batch (one GPU's shard of a
 // strong-scaling run) leaves CUs idle in each kernel; two independent kernels in flight fill
-// them.  One stream + four events per concurrent caller, from a per-device pool: a call
+// them.  One pool entry (two streams + five events) per concurrent caller, from a per-device
+// pool (the second stream carries phase C's q windows for small batches): a call
 // takes one (or creates one when all are in use) and hands it back after its last enqueue, so
 // the pool holds as many as calls ever overlapped, however many host threads come and go (a
 // thread_local stream per thread leaked one per short-lived thread: a Streamlit rerun runs on a
 // fresh ScriptRunner thread).  Reuse is safe: hipStreamWaitEvent waits on the event's record
 // at the time of the call, and the next owner's work follows on the same side stream.
 struct SideStream {
-  hipStream_t s = nullptr;
+  hipStream_t s = nullptr, s2 = nullptr;
   // fork: spectra + plan done (main); k0: full-band rows done (side); dec: decimated spectra
-  // done (main); join: the side stream's last kernel done
-  hipEvent_t fork = nullptr, k0 = nullptr, dec = nullptr, join = nullptr;
+  // done (main); join / join2: the side streams' last kernels done
+  hipEvent_t fork = nullptr, k0 = nullptr, dec = nullptr, join = nullptr, join2 = nullptr;
 };
 namespace {
 constexpr int kMaxDev = 64;
@@ -1563,13 +1564,15 @@ SideStream* side_acquire(int& dev) {
     }
   }
   SideStream* ss = new SideStream;
-  bool ok = hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) == hipSuccess;
-  for (hipEvent_t* e : {&ss->fork, &ss->k0, &ss->dec, &ss->join})
+  bool ok = hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&ss->s2, hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t* e : {&ss->fork, &ss->k0, &ss->dec, &ss->join, &ss->join2})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
-    for (hipEvent_t e : {ss->fork, ss->k0, ss->dec, ss->join})
+    for (hipEvent_t e : {ss->fork, ss->k0, ss->dec, ss->join, ss->join2})
       if (e) (void)hipEventDestroy(e);
     if (ss->s) (void)hipStreamDestroy(ss->s);
+    if (ss->s2) (void)hipStreamDestroy(ss->s2);
     delete ss;
     (void)hipGetLastError();
     return nullptr;  // the call runs single-stream
@@ -1584,15 +1587,15 @@ void side_release(SideStream* ss, int dev) {
 }
 }  // namespace
 
-// Owns a call's side stream: on every return after the fork -- success or a failed launch /
-// event call -- the side stream records `join` and the caller's stream waits on it before the
-// stream goes back to the pool, so no side-stream kernel can still be writing the workspace
-// or the outputs once the caller's stream is past the call.
+// Owns a call's side streams: on every return after a fork -- success or a failed launch /
+// event call -- each forked side stream records its join event and the caller's stream waits
+// on it before the entry goes back to the pool, so no side-stream kernel can still be writing
+// the workspace or the outputs once the caller's stream is past the call.
 struct SideJoin {
   SideStream* side = nullptr;
   hipStream_t st = nullptr;
   int dev = 0;
-  bool forked = false;
+  bool forked = false, forked2 = false;
   SideJoin(bool want, hipStream_t caller) : st(caller) {
     if (want) side = side_acquire(dev);
   }
@@ -1601,6 +1604,10 @@ struct SideJoin {
     if (forked) {
       (void)hipEventRecord(side->join, side->s);
       (void)hipStreamWaitEvent(st, side->join, 0);
+    }
+    if (forked2) {
+      (void)hipEventRecord(side->join2, side->s2);
+      (void)hipStreamWaitEvent(st, side->join2, 0);
     }
     side_release(side, dev);
   }
@@ -2044,20 +2051,20 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
   // which the side stream made, and of the decimated rows), while phase B runs here once the
   // full-band rows' time-domain rows are done; the caller's stream then joins the side stream.
   hipStream_t sc = st;
-  // option wct_pc_early: phase C's q windows on a third (pooled) stream as soon as the
+  // option wct_pc_early: phase C's q windows on the entry's second side stream as soon as the
   // decimated spectra are done -- every row of a q window is a decimated row, so they need
   // neither the full-band rows' kernel nor the spectral boxcar.  A/B (alternating, one box,
   // r04): 64 pairs 0.495 -> 0.482 ms, 128 pairs 0.843 -> 0.831, 512 pairs 3.039 -> 3.053, so
   // by default (2) for batches of at most 256 pairs
   const int pce = options().wct_pc_early;
-  SideJoin sj3(side && (pce == 1 || (pce == 2 && batch <= 256)), st);
+  const bool third = side && (pce == 1 || (pce == 2 && batch <= 256));
   if (side) {
     if (hipStreamWaitEvent(side->s, side->dec, 0) != hipSuccess) return launch_status();
     sc = side->s;
-    if (sj3.side) {
-      if (hipStreamWaitEvent(sj3.side->s, side->dec, 0) != hipSuccess) return launch_status();
-      sj3.forked = true;
-      if ((rc = phase_c(sj3.side->s, 1)) != kOk) return rc;
+    if (third) {
+      if (hipStreamWaitEvent(side->s2, side->dec, 0) != hipSuccess) return launch_status();
+      sj.forked2 = true;
+      if ((rc = phase_c(side->s2, 1)) != kOk) return rc;
     }
   }
   // spectral boxcar of the wide windows (their sums over the output rows' WB slots)
@@ -2078,7 +2085,7 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
     }
     if ((rc = launch_status()) != kOk) return rc;
   }
-  if ((rc = phase_c(sc, sj3.side ? 2 : 3)) != kOk) return rc;
+  if ((rc = phase_c(sc, third ? 2 : 3)) != kOk) return rc;
   // phase B on the caller's stream once the full-band rows are done; sj joins the side stream
   if (side && hipStreamWaitEvent(st, side->k0, 0) != hipSuccess) return launch_status();
   return wct_phase_b_any(TA, TB, batch, n0i, n_scales, out_coh, plan, boxcar, st);
@@ -2101,6 +2108,7 @@ extern "C" int wtmi_wct_morlet_norm(const float* x1, const float* x2, long long 
                          out_coh, out_power, out_phase, out_u, out_v, stream);
 }
 
-// Side streams the WCT has created in this process (all devices): the pool's size, i.e. the
-// most full-row WCT calls that ever ran at once, not the number of threads that made one.
+// Side-stream pool entries (two streams each) the WCT has created in this process (all
+// devices): the pool's size, i.e. the most full-row WCT calls that ever ran at once, not the
+// number of threads that made one.
 extern "C" long long wtmi_wct_side_streams(void) { return wtmi::side_pool().created.load(); }

@@ -94,7 +94,11 @@ def create_xwt_results_dict(xwt_data_dict: dict[str, DataForXWT], xwt_list: list
                             **kwargs) -> ResultsFromXWT:
     """run_xwt per pair (:126-135), batched: one XWT launch (+ one phase launch) per group.
     Fails as run_xwt(data, **kwargs) does in the reference: unknown keywords raise TypeError,
-    normalize=False NameError, a non-Morlet mother AttributeError."""
+    normalize=False NameError, a non-Morlet mother AttributeError -- at the first pair, after
+    its lookup (KeyError first); with no pairs the reference's loop never runs: {}."""
+    if not xwt_list:
+        return {}
+    xwt_data_dict[xwt_list[0]]
     unknown = sorted(set(kwargs) - {"normalize"})
     if unknown:
         raise TypeError(f"run_xwt() got unexpected keyword arguments {unknown}")

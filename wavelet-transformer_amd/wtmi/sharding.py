@@ -98,8 +98,9 @@ def _reduce_device(group=None) -> torch.device:
 
 def max_over_ranks(seconds: float, group=None) -> float:
     """Max of a wall time over all ranks (the bench's timed region); a host tensor under
-    gloo, a tensor on this rank's GPU under RCCL."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    gloo, a tensor on this rank's GPU under RCCL.  An initialised group of one rank still
+    runs the all-reduce (the RCCL path exercised on one GPU: bench.py --force-dist)."""
+    if not dist.is_initialized():
         return seconds
     t = torch.tensor([seconds], dtype=torch.float64, device=_reduce_device(group))
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -108,7 +109,7 @@ def max_over_ranks(seconds: float, group=None) -> float:
 
 def sum_over_ranks(value: float, group=None) -> float:
     """Sum of a scalar over all ranks (units processed), on the same device rule."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return value
     t = torch.tensor([value], dtype=torch.float64, device=_reduce_device(group))
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)

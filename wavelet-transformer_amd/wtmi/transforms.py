@@ -283,7 +283,8 @@ def wct(y1, y2, dt, dj=1 / 12, s0=-1, J=-1, sig=True, significance_level=0.95,
             J = int(np.round(np.log2(n0 * dt / s0) / dj))
         a1, _, _ = ar1(y1)
         a2, _, _ = ar1(y2)
-        kw = {k: v for k, v in kwargs.items() if k in ("cache", "mc_count", "seed", "progress", "noise")}
+        kw = {k: v for k, v in kwargs.items()
+              if k in ("cache", "mc_count", "seed", "progress", "noise", "quantile")}
         sig = wct_significance(a1, a2, dt=dt, dj=dj, s0=s0, J=J,
                                significance_level=significance_level, wavelet=wavelet, **kw)
     else:
@@ -438,10 +439,20 @@ def sig_cache_store(key, sig95) -> None:
 # from ("Monte-Carlo noise"; parity unpinned: pycwt is absent from the image).
 SIG_NOISE = os.environ.get("WTMI_SIG_NOISE", "pycwt")
 
+# Quantile step of wct_significance ("Monte-Carlo quantile"; parity unpinned):
+# "pycwt" (default) behaves as pycwt 0.4.0b0's published lines do -- its counter is
+# np.ma.zeros (never masked), so ``sel = ~wlc[s, :].mask`` is the scalar True, R2y[sel] is
+# 2-D and np.interp raises ValueError("object too deep for desired array") under numpy 1.26.4
+# (the reference's pin) and 2.x; "nonempty" is the engine's alternative: the levels
+# interpolated over each scale's non-empty bins (ops.coherence_quantile).
+QUANTILE_MODES = ("pycwt", "nonempty")
+SIG_QUANTILE = os.environ.get("WTMI_SIG_QUANTILE", "pycwt")
+PYCWT_QUANTILE_ERROR = "object too deep for desired array"
+
 
 def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="morlet",
                      mc_count=300, progress=True, cache=True, seed=None, nbins=1000,
-                     max_pairs_per_launch=512, noise=None):
+                     max_pairs_per_launch=512, noise=None, quantile=None):
     """pycwt ``wct_significance`` on the GPU: mc_count passes of two noise series
     (helpers.rednoise with al1, al2; ``noise`` "pycwt" or "red", default ``SIG_NOISE``),
     their coherence, and the per-scale counter of floor(R2 * nbins) outside the COI, batched
@@ -449,24 +460,37 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     in process memory and on disk (``sig_cache_dir()``), as pycwt's ``cache=True`` keeps them
     under the user cache dir (src/wct.py:117); ``seed`` None draws a fresh one, as pycwt's
     unseeded draws do.  Like pycwt's rednoise (whose g == 0 branch calls the nonexistent
-    ``np.randn``), a zero lag-1 coefficient raises AttributeError in the "pycwt" mode."""
+    ``np.randn``), a zero lag-1 coefficient raises AttributeError in the "pycwt" mode.
+    ``quantile`` ("pycwt" or "nonempty", default ``SIG_QUANTILE``): in the "pycwt" mode the
+    call raises ValueError as pycwt's quantile step does once maxscale > 0 (pycwt raises it
+    after its mc_count passes and before it writes its cache; the passes change nothing
+    observable, so they are not run)."""
     wavelet = as_morlet(wavelet)
     if wavelet.deltaj0 <= 0:
         raise ValueError("wct_significance needs a Morlet(6) wavelet (deltaj0 defined)")
     noise = SIG_NOISE if noise is None else noise
     if noise not in ops.NOISE_MODES:
         raise ValueError(f"noise must be one of {ops.NOISE_MODES}, got {noise!r}")
-    if noise == "pycwt" and (float(al1) == 0.0 or float(al2) == 0.0):
+    quantile = SIG_QUANTILE if quantile is None else quantile
+    if quantile not in QUANTILE_MODES:
+        raise ValueError(f"quantile must be one of {QUANTILE_MODES}, got {quantile!r}")
+    if noise == "pycwt" and int(mc_count) > 0 and (float(al1) == 0.0 or float(al2) == 0.0):
         raise AttributeError("module 'numpy' has no attribute 'randn' "
                              "(pycwt helpers.rednoise with g == 0)")
+    N, sj, t_lo, t_hi, anyout, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
+    if quantile == "pycwt" and maxscale > 0:
+        raise ValueError(f"{PYCWT_QUANTILE_ERROR} (pycwt 0.4.0b0 wct_significance: np.interp "
+                         "over the unmasked np.ma counter; quantile='nonempty' or "
+                         "WTMI_SIG_QUANTILE=nonempty gives the levels)")
+    # the key holds the exact lag-1 coefficients (pycwt's cache name rounds arctanh(4 al),
+    # NaN for |al| > 0.25; DESIGN 4)
     cache = cache and SIG_CACHE
-    key = ("wct_significance", 2, noise, float(al1), float(al2), float(dt), float(dj), float(s0),
-           int(J), float(significance_level), wavelet.f0, int(mc_count), int(nbins), seed)
+    key = ("wct_significance", 3, noise, quantile, float(al1), float(al2), float(dt), float(dj),
+           float(s0), int(J), float(significance_level), wavelet.f0, int(mc_count), int(nbins), seed)
     if cache:
         hit = sig_cache_load(key)
         if hit is not None:
             return hit
-    N, sj, t_lo, t_hi, anyout, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
     if N > ops.MAX_SAMPLES:
         raise ValueError(f"wct_significance: noise length {N} exceeds the engine's "
                          f"{ops.MAX_SAMPLES} samples per row")
