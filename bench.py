@@ -308,7 +308,7 @@ class C3(Workload):
     """MODWT db4 J=10: 8192 x 16384, decompose + reconstruct."""
     name, axis, seed = "c3", "series", 1003
     B, n, J = 8192, 16384, 10
-    kernel = "modwt_vec_kernel<8,4,1024,16>+imodwt_hyb_kernel<8,8,512,2,4>"
+    kernel = "modwt_vec_kernel<8,4,1024,16>+imodwt_hyb_kernel<8,8,512,2,1024>"
     PER_STEP = {"wtmi::modwt_vec_kernel<": 1, "wtmi::imodwt_hyb_kernel<": 1}
 
     def setup(self):

@@ -200,12 +200,13 @@ def test_wavedec_batched_vs_oracle():
         assert np.abs(ct[b] - ref).max() <= TOL * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("syn", [1, 0])
+@pytest.mark.parametrize("syn", [1, 2, 0])
 @pytest.mark.parametrize("n,J", [(16384, 10), (16384, 15), (8192, 12), (4096, 3)])
 def test_imodwt_adjoint_and_masks_at_bench_shape(n, J, syn, db4):
     """Synthesis on NON-range input (adjoint, every tap exercised) and with row masks at
-    the C3 shape vs the textbook oracle, for both n = 16384 kernels (option modwt_syn: 1 the
-    hybrid with LDS-staged low levels, 0 dilation chains only).  J = 15 reaches dilations
+    the C3 shape vs the textbook oracle, for the n = 16384 / 8192 kernels (option modwt_syn: 1
+    the hybrid with every level staged through LDS, 2 the hybrid with chain levels from L2,
+    0 dilation chains only).  J = 15 reaches dilations
     past the chain range (2^12 samples) and 2^14 = 0 mod n."""
     from wtmi import _lib
     rng = np.random.default_rng(n + J)

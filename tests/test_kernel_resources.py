@@ -26,7 +26,8 @@ BUDGET = {
     # C3 analysis: one 1024-thread workgroup per series, two per CU (64 KiB of LDS each) = 8
     # waves per SIMD, so at most 64 VGPRs (r04: an extra code path at 68 would halve occupancy)
     "void wtmi::modwt_vec_kernel<8, 4, 1024, 16>": 64,
-    "void wtmi::imodwt_hyb_kernel<8, 8, 512, 2, 4>": 128,  # C3 synthesis: two workgroups / CU
+    "void wtmi::imodwt_hyb_kernel<8, 8, 512, 2, 1024>": 128,  # C3 synthesis: two workgroups / CU
+    "void wtmi::imodwt_hyb_kernel<8, 8, 512, 2, 4>": 128,
 }
 BUDGET.update({f"void wtmi::wct_dec_kernel<13, {m}>": 128 for m in range(8, 13)})
 BUDGET["void wtmi::wct_dec_merged<13>"] = 128  # C4 decimation classes M = 4096 .. 512, one launch

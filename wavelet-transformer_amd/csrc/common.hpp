@@ -167,7 +167,8 @@ struct Options {
   int wct_target_wg = 0;    // WTMI_WCT_TARGET_WG: 0 = as many as wct_min_rows allows
   int wct_min_rows = 0;     // WTMI_WCT_MIN_ROWS: scale rows per WCT workgroup, at least (0 = by batch)
   int wct_dec_rows = 0;     // WTMI_WCT_DEC_ROWS: decimated scale rows per phase A workgroup (0 = by batch)
-  int modwt_syn = 1;        // WTMI_MODWT_SYN: 1 hybrid synthesis (low levels via LDS), 0 MODE 3 only
+  int modwt_syn = 1;        // WTMI_MODWT_SYN: 1 hybrid synthesis, every level via LDS (r05); 2 the
+                            // same with chain levels dq >= 4 groups from L2 (r04); 0 MODE 3 only
   int wct_wide = 1;         // WTMI_WCT_WIDE: windows of union band N >> e take the spectral route
                             // from e >= wct_wide (1..3); 0 = never (time path)
   int modwt_ana = 0;        // WTMI_MODWT_ANA: n = 16384 analysis with 1024 threads x 4 groups (0),

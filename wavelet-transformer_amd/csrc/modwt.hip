@@ -971,10 +971,19 @@ extern "C" int wtmi_imodwt(const float* w, long long batch, long long n, const d
       launch(imodwt_vec_kernel<8, 1, 512, 0>, 512);
     else if (ng <= 1024)
       launch(imodwt_vec_kernel<8, 1, 1024, 0>, 1024);
-    else if (ng == 4096 && options().modwt_syn == 1)  // C3 A/B on one box, two orders: 1.24 ms vs
-      // 1.41-1.52 (MODE 3); global chains from dq >= 2: 1.27-1.43, from dq >= 8 1.21-1.32
+    // n = 16384 / 8192: the hybrid synthesis.  r05: every level's W_j staged through LDS
+    // (CG = 1024 > any dilation; r04 kept W_j taps of the chain levels dq >= 4 groups in L2).
+    // FETCH per C3 launch 6.50 -> 5.91 GB = exactly the 11 rows (the L2 taps shared by
+    // neighbouring chains were partly re-fetched), 1.269-1.274 -> 1.234-1.239 ms in one
+    // process, 4 alternations (profiles/r05/c3_syn_cg.txt; CG 8 / 16 / 32 / 64 in between).
+    // modwt_syn 2 keeps r04's CG = 4.
+    else if (ng == 4096 && options().modwt_syn == 1)
+      launch_lds(imodwt_hyb_kernel<8, 8, 512, 2, 1024>, 512, lds_pad);
+    else if (ng == 4096 && options().modwt_syn == 2)
       launch_lds(imodwt_hyb_kernel<8, 8, 512, 2, 4>, 512, lds_pad);
     else if (ng == 2048 && options().modwt_syn == 1)
+      launch_lds(imodwt_hyb_kernel<8, 4, 512, 2, 1024>, 512, lds_pad);
+    else if (ng == 2048 && options().modwt_syn == 2)
       launch_lds(imodwt_hyb_kernel<8, 4, 512, 2, 4>, 512, lds_pad);
     else if (ng <= 2048)
       launch_lds(imodwt_vec_kernel<8, 2, 1024, 3>, 1024, lds_pad);

@@ -19,7 +19,7 @@ constexpr Entry kEntries[] = {
     {"wct_target_wg", &Options::wct_target_wg, 0, 1 << 24},
     {"wct_min_rows", &Options::wct_min_rows, 0, 1 << 10},
     {"wct_dec_rows", &Options::wct_dec_rows, 0, 128},
-    {"modwt_syn", &Options::modwt_syn, 0, 1},
+    {"modwt_syn", &Options::modwt_syn, 0, 2},
     {"modwt_ana", &Options::modwt_ana, 0, 2},
     {"wct_wide", &Options::wct_wide, 0, 4},
     {"wct_side_stream", &Options::wct_side_stream, 0, 1},
