@@ -25,6 +25,7 @@ constexpr Entry kEntries[] = {
     {"wct_side_stream", &Options::wct_side_stream, 0, 1},
     {"wct_pc_early", &Options::wct_pc_early, 0, 2},
     {"wct_dec_merge", &Options::wct_dec_merge, 0, 2},
+    {"wct_depth", &Options::wct_depth, 0, 1},
 };
 
 // Process defaults: the environment, read once (immutable afterwards).
@@ -61,7 +62,7 @@ const Options& options() { return thread_options(); }
 
 // Set a launch option by name (cwt_prune, cwt_target_wg, wct_prune, wct_target_wg,
 // wct_min_rows, wct_dec_rows, modwt_syn, modwt_ana, wct_wide, wct_side_stream, wct_pc_early,
-// wct_dec_merge) for the CALLING
+// wct_dec_merge, wct_depth) for the CALLING
 // thread.  0 on success, -1 unknown
 // name or out of range.  Applies to launches this thread issues after the call; other
 // threads keep their own values (the process defaults come from WTMI_<NAME>).

@@ -1123,7 +1123,7 @@ template <int C> struct ColVec;
 template <> struct ColVec<1> { using T = float2; };
 template <> struct ColVec<2> { using T = float4; };
 
-template <int K, int C>
+template <int K, int C, int DD = 0>
 __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, const cpx* __restrict__ TB,
                                                    long long batch, int n0, int S, float* __restrict__ coh,
                                                    const int* __restrict__ plan) {
@@ -1153,8 +1153,8 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
   const int jend = last + HI + 1;  // output rows i = j - HI <= last
   const int jlim = min(S, jend);   // rows read
   // Rows are loaded D ahead of their use (D | K, so the pending slot of row jb + r is r % D):
-  // D rows of loads in flight per thread instead of one.
-  constexpr int D = (K % 6 == 0) ? 6 : (K % 5 == 0) ? 5 : (K % 4 == 0) ? 4 : (K % 3 == 0) ? 3 : (K % 2 == 0) ? 2 : 1;
+  // D rows of loads in flight per thread instead of one (DD: forced depth, option wct_depth).
+  constexpr int D = DD ? DD : (K % 6 == 0) ? 6 : (K % 5 == 0) ? 5 : (K % 4 == 0) ? 4 : (K % 3 == 0) ? 3 : (K % 2 == 0) ? 2 : 1;
   V pa[D], pc[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
 // covers k) and, once output row i's window is complete, writes the window sums over row i's
 // own WB slot (bin k, in place: only this thread reads or writes index k, and row i's own bins
 // were read before).  Rows outside [0, S) and bins past a row's band count as zero.
-template <int K>
+template <int K, int DD = 0>
 __global__ void __launch_bounds__(256) wct_wide_boxcar(cpx* __restrict__ WB, long long batch, int N, int S,
                                                        const int* __restrict__ plan) {
   const int nb = N / 2;  // bins per slot
@@ -1361,7 +1361,7 @@ __global__ void __launch_bounds__(256) wct_wide_boxcar(cpx* __restrict__ WB, lon
   };
   // rows are loaded D ahead of their use (D | K: the pending slot of row jb + q is q % D), so D
   // rows of loads are in flight per thread; the sums' stores follow the loads they overtake
-  constexpr int D = (K % 6 == 0) ? 6 : (K % 5 == 0) ? 5 : (K % 4 == 0) ? 4 : (K % 3 == 0) ? 3 : (K % 2 == 0) ? 2 : 1;
+  constexpr int D = DD ? DD : (K % 6 == 0) ? 6 : (K % 5 == 0) ? 5 : (K % 4 == 0) ? 4 : (K % 3 == 0) ? 3 : (K % 2 == 0) ? 2 : 1;
   cpx pz[D], pw[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) load(jlo + d, pz[d], pw[d]);
@@ -1749,8 +1749,12 @@ static int launch_phase_b(const cpx* TA, const cpx* TB, long long batch, int n0,
   const long long tiles = (static_cast<long long>(n0) + 255) / 256;
   const long long grid = batch * tiles;
   if (grid > 0x7fffffffll) return kErrUnsupported;
-  hipLaunchKernelGGL((wct_phase_b<K, 1>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
-                     batch, n0, S, coh, plan);
+  if (K <= 12 && options().wct_depth == 1)
+    hipLaunchKernelGGL((wct_phase_b<K, 1, (K <= 12 ? K : 0)>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
+                       batch, n0, S, coh, plan);
+  else
+    hipLaunchKernelGGL((wct_phase_b<K, 1>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, TA, TB,
+                       batch, n0, S, coh, plan);
   return launch_status();
 }
 
@@ -2074,6 +2078,10 @@ static int wct_morlet_impl(const float* x1, const float* x2, long long ld, long 
     switch (boxcar) {
 #define WTMI_W(KK)                                                                                         \
   case KK:                                                                                                 \
+    if (KK <= 12 && options().wct_depth == 1)                                                              \
+      hipLaunchKernelGGL((wct_wide_boxcar<KK, (KK <= 12 ? KK : 0)>), dim3(static_cast<unsigned>(batch * tiles)), dim3(256), 0, sc, WB, \
+                         batch, 1 << logn, n_scales, plan);                                               \
+    else                                                                                                   \
     hipLaunchKernelGGL(wct_wide_boxcar<KK>, dim3(static_cast<unsigned>(batch * tiles)), dim3(256), 0, sc, WB, \
                        batch, 1 << logn, n_scales, plan);                                                 \
     break;
