@@ -21,8 +21,10 @@ BUDGET = {
     "void wtmi::wct_phase_a<13, true, 2>": 128,          # C4 decimated rows
     "void wtmi::wct_phase_c<13, true, false>": 128,      # C4 q windows
     "void wtmi::wct_phase_c<13, true, true>": 128,       # C4 wide windows
-    "void wtmi::wct_phase_b<10, 1>": 128,
-    "void wtmi::wct_wide_boxcar<10>": 128,
+    "void wtmi::wct_phase_b<10, 1, 10>": 128,            # r05 default: K rows in flight
+    "void wtmi::wct_wide_boxcar<10, 10>": 128,
+    "void wtmi::wct_phase_b<10, 1, 0>": 128,
+    "void wtmi::wct_wide_boxcar<10, 0>": 128,
     # C3 analysis: one 1024-thread workgroup per series, two per CU (64 KiB of LDS each) = 8
     # waves per SIMD, so at most 64 VGPRs (r04: an extra code path at 68 would halve occupancy)
     "void wtmi::modwt_vec_kernel<8, 4, 1024, 16>": 64,

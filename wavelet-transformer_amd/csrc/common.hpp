@@ -181,8 +181,10 @@ struct Options {
   int wct_dec_merge = 2;    // WTMI_WCT_DEC_MERGE: the decimation classes M = 4096 .. 512 in one
                             // launch (1), one launch per class (0), or the former for batches of
                             // at most 256 pairs (2)
-  int wct_depth = 0;        // WTMI_WCT_DEPTH: rows in flight per thread of phase B and the wide
-                            // boxcar: the largest of 6..1 dividing K (0) or K itself (1, K <= 12)
+  int wct_depth = 1;        // WTMI_WCT_DEPTH: rows in flight per thread of phase B and the wide
+                            // boxcar: K itself (1, K <= 12; r05) or the largest of 6..1 dividing
+                            // K (0, r04).  C4 serial trace: phase B 0.2935 -> 0.2840 ms, boxcar
+                            // 0.2538 -> 0.2515; 64-pair step 0.4499 -> 0.4434 (alternating)
 };
 const Options& options();
 
