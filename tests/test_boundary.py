@@ -321,3 +321,24 @@ def test_overlay_run_cli(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("ARGS")][0]
     assert "['x', '--flag']" in line and os.path.join(PKG, "src", "cwt.py") in line
+
+
+def test_rows_gives_the_abi_a_valid_row_stride():
+    """The C ABI rejects ld < n.  A one-row view may carry any batch stride in torch (NumPy's
+    x[None, :] arrives with stride 0), an expanded batch has stride 0: ops._rows re-strides or
+    copies both, so wtmi_modwt & co. never see an invalid ld (found by the random-shape sweep)."""
+    import numpy as np
+    import torch
+    from wtmi import ops
+    t = torch.tensor(np.arange(8, dtype=np.float32)[None, :])
+    assert t.stride(0) == 0
+    r = ops._rows(t)
+    assert r.stride() == (8, 1) and torch.equal(r, t)
+    r = ops._rows(torch.tensor(np.arange(8.0)[None, :]), torch.float32)
+    assert r.stride() == (8, 1) and r.dtype == torch.float32
+    r = ops._rows(torch.arange(5.0).expand(3, 5))
+    assert r.stride() == (5, 1)
+    r = ops._rows(torch.arange(10.0)[::2])
+    assert r.stride() == (5, 1) and r.tolist() == [[0.0, 2.0, 4.0, 6.0, 8.0]]
+    r1, r2 = ops._pair_rows(torch.zeros(4, 16)[:, :8], torch.zeros(4, 8))
+    assert r1.stride(0) == r2.stride(0)

@@ -45,14 +45,21 @@ def _check_dev(*ts):
     return dev
 
 
-def _rows(x: torch.Tensor) -> torch.Tensor:
-    """[n] or [B, n] -> [B, n] with unit stride along time."""
+def _rows(x: torch.Tensor, dtype=None) -> torch.Tensor:
+    """[n] or [B, n] -> [B, n] with unit stride along time and a row stride >= n (the C ABI's
+    ld).  A size-1 batch dimension may carry any stride in torch (NumPy's x[None, :] arrives
+    with stride 0), so a one-row view is re-strided to ld = n; an expanded batch is copied."""
+    if dtype is not None:
+        x = x.to(dtype)
     if x.dim() == 1:
         x = x.unsqueeze(0)
     if x.dim() != 2:
         raise ValueError("expected a [batch, n] tensor")
-    if x.stride(1) != 1:
+    B, n = x.shape
+    if x.stride(1) != 1 or (B > 1 and x.stride(0) < n):
         x = x.contiguous()
+    if B == 1 and x.stride(0) != n:
+        x = x.as_strided((1, n), (n, 1), x.storage_offset())
     return x
 
 
@@ -92,7 +99,7 @@ def series_moments(x: torch.Tensor) -> torch.Tensor:
     x = _rows(x)
     dev = _check_dev(x)
     if x.dtype not in (torch.float32, torch.float64):
-        x = x.to(torch.float64)
+        x = _rows(x, torch.float64)
     out = torch.empty((x.shape[0], 8), dtype=torch.float64, device=dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_series_moments", _ptr(x), int(x.dtype == torch.float64), x.stride(0),
@@ -112,7 +119,7 @@ def series_affine(x: torch.Tensor, mode: int = AFF_NORMALIZE) -> torch.Tensor:
     x = _rows(x)
     dev = _check_dev(x)
     if x.dtype not in (torch.float32, torch.float64):
-        x = x.to(torch.float64)
+        x = _rows(x, torch.float64)
     out = torch.empty((x.shape[0], 3), dtype=torch.float64, device=dev)
     with torch.cuda.device(dev):
         _lib.call("wtmi_series_affine", _ptr(x), int(x.dtype == torch.float64), x.stride(0),
@@ -125,7 +132,7 @@ def affine(x: torch.Tensor, coef: torch.Tensor, dtype=torch.float32) -> torch.Te
     x = _rows(x)
     dev = _check_dev(x, coef)
     if x.dtype not in (torch.float32, torch.float64):
-        x = x.to(torch.float64)
+        x = _rows(x, torch.float64)
     coef = coef.to(torch.float64).contiguous()
     y = torch.empty(x.shape, dtype=dtype, device=dev)
     with torch.cuda.device(dev):
@@ -214,8 +221,7 @@ def cwt_morlet(x: torch.Tensor, scales, dt: float, f0: float = 6.0, *,
     if not (want_w or want_power or want_sig):
         raise ValueError("cwt_morlet: no output requested")
     dev = _check_dev(x, affine, out_w)
-    if x.dtype != torch.float32:
-        x = x.to(torch.float32)
+    x = _rows(x, torch.float32)
     sc = _f64_dev(scales, dev)
     ss = _f64_dev(sig_scale, dev) if want_sig else None
     aff = _f64_arg(affine, dev)
@@ -254,8 +260,8 @@ def _long_workspace(B, n0, S, pair, dev):
 
 
 def _pair_rows(x1, x2):
-    x1 = _rows(x1).to(torch.float32)
-    x2 = _rows(x2).to(torch.float32)
+    x1 = _rows(x1, torch.float32)
+    x2 = _rows(x2, torch.float32)
     if x1.shape != x2.shape:
         raise ValueError("x1 and x2 must have the same shape")
     if x1.stride(0) != x2.stride(0):
@@ -439,7 +445,7 @@ def _out(out, shape, dev):
 
 def modwt(x: torch.Tensor, dec_lo, dec_hi, level: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[B, n] float32 -> [B, level + 1, n] rows [W_1 .. W_J, V_J]."""
-    x = _rows(x).to(torch.float32)
+    x = _rows(x, torch.float32)
     dev = _check_dev(x)
     B, n = x.shape
     lo, hi = _taps(dec_lo), _taps(dec_hi)
@@ -487,7 +493,7 @@ def dwt_lengths(n: int, n_taps: int, level: int) -> list:
 
 def wavedec(x: torch.Tensor, dec_lo, dec_hi, level: int):
     """Returns (coeffs [B, total] float32 in pywt order, lens)."""
-    x = _rows(x).to(torch.float32)
+    x = _rows(x, torch.float32)
     dev = _check_dev(x)
     B, n = x.shape
     lo, hi = _taps(dec_lo), _taps(dec_hi)
