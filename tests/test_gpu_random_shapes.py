@@ -145,3 +145,73 @@ def test_random_modwt_and_dwt_match_oracle(case, filters):
     rec = ops.waverec(coeffs, n, fb["rec_lo"], fb["rec_hi"], level, [(1 << (level + 1)) - 1]).cpu().numpy()
     for b in range(B):
         gate(f"waverec[{b}]", np.abs(rec[b, 0, :n] - x[b]).max() / np.abs(x[b]).max())
+
+
+def _xwt_cases(seed=404, count=10):
+    rng = np.random.default_rng(seed)
+    mothers = [None, pc.Paul(4), pc.DOG(2), pc.MexicanHat(), pc.DOG(3), pc.Paul(6)]
+    out = []
+    for i in range(count):
+        n0 = int(np.exp(rng.uniform(np.log(12), np.log(16384))))
+        dj = float(rng.choice([1 / 4, 1 / 8, 1 / 12]))
+        m = mothers[i % len(mothers)]
+        out.append((i, n0, dj, m))
+    return out
+
+
+def _mname(m):
+    return "morlet" if m is None else f"{m.name}{getattr(m, 'm', '')}"
+
+
+@pytest.mark.parametrize("case", _xwt_cases(), ids=lambda c: f"xwt{c[0]}-{_mname(c[3])}-n{c[1]}")
+def test_random_xwt_pair_and_mothers_match_oracle(case):
+    """The XWT pair kernel (W12, |W12|^2, significance ratio) and the non-Morlet mothers of the
+    reference's MOTHER_DICT (Paul, DOG, Mexican hat; VAR = 1 kernels) at random shapes."""
+    from wtmi import ops
+    i, n0, dj, mother = case
+    rng = np.random.default_rng(4000 + i)
+    B = 2
+    y1 = np.stack([red_series(rng, n0) for _ in range(B)])
+    y2 = (0.6 * np.roll(y1, 3, axis=1) + 0.8 * np.stack([red_series(rng, n0) for _ in range(B)])
+          ).astype(np.float32)
+    dt, s0 = 1 / 12, 2 / 12
+    wl = mother or pc.Morlet(6)
+    J = max(1, min(int(np.round(np.log2(n0 * dt / s0) / dj)), 120))
+    sj = s0 * 2 ** (np.arange(J + 1) * dj)
+    ss = np.linspace(0.5, 2.0, sj.size)
+    r = ops.xwt_morlet(torch.tensor(y1, device="cuda"), torch.tensor(y2, device="cuda"), sj, dt,
+                       sig_scale=ss, want_w12=True, want_power=True, want_sig=True,
+                       mother=mother)
+    for b in range(B):
+        W1 = pc.cwt(y1[b].astype(np.float64), dt, dj, s0, J, wl)[0]
+        W2 = pc.cwt(y2[b].astype(np.float64), dt, dj, s0, J, wl)[0]
+        W12 = W1 * W2.conj()
+        # rows where the reference carries energy (Paul rows of a short series at the largest
+        # scales can vanish to the fp64 floor, as in test_gpu_mothers)
+        nrm = np.linalg.norm(W12, axis=-1)
+        keep = nrm > 1e-6 * nrm.max()
+        g = r["w12"][b].cpu().numpy().astype(np.complex128)
+        gate(f"W12[{b}]", row_relerr(g[keep], W12[keep]))
+        p = r["power"][b].cpu().numpy().astype(np.float64)
+        gate(f"xwt power[{b}]", row_relerr(p[keep], (np.abs(W12) ** 2)[keep]))
+        sg = r["sig"][b].cpu().numpy().astype(np.float64)
+        gate(f"xwt sig ratio[{b}]", row_relerr(sg[keep], (np.abs(W12) ** 2 * ss[:, None])[keep]))
+
+
+@pytest.mark.parametrize("case", _filter_ids()[:8], ids=lambda c: f"mra{c[0]}-{c[2]}-n{c[1]}")
+def test_random_modwt_masks_match_oracle(case, filters):
+    """MODWT multiresolution pieces (imodwt with a row keep-mask, the engine's MRA / smoothing
+    path) at random lengths and filter banks against the oracle's masked synthesis."""
+    from wtmi import ops
+    i, n, name = case
+    fb = {k: np.asarray(v) for k, v in filters[name].items()}
+    rng = np.random.default_rng(5000 + i)
+    x = red_series(rng, n)[None, :]
+    J = int(rng.integers(1, max(2, min(10, int(np.log2(n)) - 1))))
+    C = ops.modwt(torch.tensor(x, device="cuda"), fb["dec_lo"], fb["dec_hi"], J)
+    Ch = C.cpu().numpy().astype(np.float64)[0]
+    for keep in (1 << J, 1, (1 << (J + 1)) - 2, int(rng.integers(1, 1 << (J + 1)))):
+        got = ops.imodwt(C, fb["dec_lo"], fb["dec_hi"], keep).cpu().numpy()[0]
+        wm = Ch * np.array([(keep >> r) & 1 for r in range(J + 1)])[:, None]
+        ref = ms.imodwt_direct(wm, fb["dec_lo"], fb["dec_hi"])
+        gate(f"masked imodwt keep={keep:#x}", np.abs(got - ref).max() / max(np.abs(Ch).max(), 1e-30), 3e-5)
