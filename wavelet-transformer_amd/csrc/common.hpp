@@ -123,22 +123,35 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
   void* q = reinterpret_cast<void*>((static_cast<unsigned long long>(hi) << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(q, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+// Cache policy operand (aux) of the buffer loads / stores: 0 = default, kNt = streaming (nt).
+// Measured per kernel (profiles/r05/nt_policy_ab.txt): nt on the once-read rows of the MODWT
+// synthesis and on the WCT kernels' row stores pays; on the CWT's output stream it costs 2-3 %.
+constexpr int kNt = 2;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// a once-read float4 row element through a plain pointer, streaming policy
+__device__ __forceinline__ float4 ld_nt4(const float4* p) {
+  return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p)));
 }
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+template <int AUX = 0>
+__device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, AUX);
+}
+template <int AUX = 0>
 __device__ __forceinline__ void buf_st(cpx v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, AUX);
 }
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <int AUX = 0>
 __device__ __forceinline__ void buf_st(float4 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, AUX);
 }
 __device__ __forceinline__ float buf_ld_f32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
+template <int AUX = 0>
 __device__ __forceinline__ cpx buf_ld_c64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(cpx, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  return __builtin_bit_cast(cpx, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX));
 }
 
 // Bijective XCD-aware block remap (CDNA guide T1).  The dispatcher deals blocks

@@ -317,7 +317,7 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
   {
     float4 xv[GROUPS];  // every load in flight before the first LDS write
 #pragma unroll
-    for (int k = 0; k < GROUPS; ++k) xv[k] = xin[min(tid + k * T, ng - 1)];
+    for (int k = 0; k < GROUPS; ++k) xv[k] = ld_nt4(&xin[min(tid + k * T, ng - 1)]);
 #pragma unroll
     for (int k = 0; k < GROUPS; ++k) {
       pin4(xv[k]);  // not sunk into the guarded store (that re-serialises the loads)
@@ -652,7 +652,7 @@ __global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 
     const float4* vr = row4(level);
     float4 vin[GROUPS];
 #pragma unroll
-    for (int k = 0; k < GROUPS; ++k) vin[k] = vr[tid + k * T];
+    for (int k = 0; k < GROUPS; ++k) vin[k] = ld_nt4(&vr[tid + k * T]);
     const bool keepV = kept(level);
 #pragma unroll
     for (int k = 0; k < GROUPS; ++k) {
@@ -686,8 +686,12 @@ __global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 
     v4f wreg[GROUPS];  // native vectors: float4 copies of loads became stack arrays
     {
       const v4f* wv = reinterpret_cast<const v4f*>(useW ? wr : row4(level));
+      // buffer loads off the wave-uniform row, streaming policy (each W_j is read once): C3
+      // 2.55 -> 2.47 ms against plain global loads (2.50 as default-policy buffer loads)
+      const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(wv);
 #pragma unroll
-      for (int k = 0; k < GROUPS; ++k) wreg[k] = wv[tid + k * T];
+      for (int k = 0; k < GROUPS; ++k)
+        wreg[k] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rw, 16 * tid, 16 * k * T, kNt));
     }
     const int q0 = chain ? chain_q0<GROUPS>(tl, dqlog) : 0;
     auto phase = [&](const float* c, bool first) {

@@ -31,6 +31,29 @@
 
 namespace wtmi {
 
+// Cache policy of the WCT's streamed accesses, a bit mask (WTMI_WCT_NT: build knob for A/B runs):
+//   1 output rows (power, phase, arrows, phase C coherence), 2 time-path rows T, 4 WB rows,
+//   8 phase B's coherence stores, 16 band_load reads (DY, TA, TB), 32 phase B's reads of T,
+//   64 the decimation kernels' stores (DY, SB, T, WB), 128 the wide boxcar's reads and writes of
+//   WB, 256 phase C's reads of SB and WB
+#ifndef WTMI_WCT_NT
+#define WTMI_WCT_NT 191
+#endif
+constexpr int kWctNt = WTMI_WCT_NT;
+template <int BIT> constexpr int wct_aux() { return (kWctNt & BIT) ? kNt : 0; }
+template <int BIT> __device__ __forceinline__ void st_c(cpx* p, cpx v) {
+  if constexpr (wct_aux<BIT>() != 0)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+template <int BIT> __device__ __forceinline__ cpx ld_c(const cpx* p) {
+  if constexpr (wct_aux<BIT>() != 0)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
 template <int LOGN>
 struct WctGeom {
   using P = FftPlan<LOGN>;
@@ -127,7 +150,7 @@ __device__ __forceinline__ void load_spec(cpx (&X)[16], const cpx* row, int t) {
 // FULL: the full-row kernels (n0 = N) compile only the unmasked loop, the padded-row kernels
 // (launched for n0 < N) only the masked one -- a runtime choice between two copies of the
 // store loop cost phase A registers (48 -> 140 spilled bytes per lane).
-template <int LOGN, bool BUF, bool FULL, typename T, typename F>
+template <int LOGN, bool BUF, bool FULL, int AUX = 0, typename T, typename F>
 __device__ __forceinline__ void put_row(T* row, int t, int n0, F&& val) {
   using P = FftPlan<LOGN>;
   if constexpr (BUF) {
@@ -135,13 +158,13 @@ __device__ __forceinline__ void put_row(T* row, int t, int n0, F&& val) {
     const __amdgpu_buffer_rsrc_t r = uniform_rsrc(row, n0 * SZ);
     if constexpr (FULL) {
 #pragma unroll
-      for (int m = 0; m < 16; ++m) buf_st(val(m), r, SZ * t, SZ * m * P::NT);
+      for (int m = 0; m < 16; ++m) buf_st<AUX>(val(m), r, SZ * t, SZ * m * P::NT);
     } else {
       int tt = t;  // per row, not hoisted out of the caller's row loop (16 live selects)
       asm volatile("" : "+v"(tt));
 #pragma unroll
       for (int m = 0; m < 16; ++m)
-        buf_st(val(m), r, tt + m * P::NT < n0 ? SZ * t : SZ * n0, SZ * m * P::NT);
+        buf_st<AUX>(val(m), r, tt + m * P::NT < n0 ? SZ * t : SZ * n0, SZ * m * P::NT);
     }
   } else {
 #pragma unroll
@@ -253,20 +276,20 @@ __device__ __forceinline__ int wct_regime(double s, double dt, double f0, double
 template <int LOGN, bool BUF, bool FULL>
 __device__ __forceinline__ void xwt_outputs(const CwtArgs& a, const cpx (&w)[16], long long rowbase, int t) {
   const int n0 = a.n0;
-  if (a.out_pow) put_row<LOGN, BUF, FULL>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w[m]); });
+  if (a.out_pow) put_row<LOGN, BUF, FULL, wct_aux<1>()>(a.out_pow + rowbase, t, n0, [&](int m) { return cabs2(w[m]); });
   if (a.out_sig) {  // phase angle, two positions per packed polynomial
     cpx ang[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m)
       ang[m] = fast_atan2f_x2(cpx{w[2 * m].y, w[2 * m + 1].y}, cpx{w[2 * m].x, w[2 * m + 1].x});
-    put_row<LOGN, BUF, FULL>(a.out_sig + rowbase, t, n0, [&](int m) { return ang[m >> 1][m & 1]; });
+    put_row<LOGN, BUF, FULL, wct_aux<1>()>(a.out_sig + rowbase, t, n0, [&](int m) { return ang[m >> 1][m & 1]; });
   }
   if (a.out_u) {
-    put_row<LOGN, BUF, FULL>(a.out_u + rowbase, t, n0, [&](int m) {
+    put_row<LOGN, BUF, FULL, wct_aux<1>()>(a.out_u + rowbase, t, n0, [&](int m) {
       const float r = sqrtf(cabs2(w[m]));
       return r > 0.f ? w[m].y / r : 0.f;
     });
-    put_row<LOGN, BUF, FULL>(a.out_v + rowbase, t, n0, [&](int m) {
+    put_row<LOGN, BUF, FULL, wct_aux<1>()>(a.out_v + rowbase, t, n0, [&](int m) {
       const float r = sqrtf(cabs2(w[m]));
       return r > 0.f ? w[m].x / r : 1.f;
     });
@@ -491,8 +514,9 @@ template <int LOGN>
 __device__ __forceinline__ cpx* wb_row(cpx* WB, long long b, int S, int j, int f) {
   return WB + ((b * S + j) * 2 + f) * static_cast<long long>(FftPlan<LOGN>::N / 2) + FftPlan<LOGN>::N / 4;
 }
+template <int BIT = 4>
 __device__ __forceinline__ void wb_put(cpx* row, int mw, int k, cpx y) {
-  if (k >= -(mw >> 1) && k < (mw >> 1)) row[k] = y;
+  if (k >= -(mw >> 1) && k < (mw >> 1)) st_c<BIT>(row + k, y);
 }
 // The whole smoothed spectrum of a thread (bins t + (m < 8 ? m : m - 16) NT) into a WB slot.
 // Rows owned by whole waves (NT >= 64) store through a wave-uniform buffer descriptor: one
@@ -510,7 +534,7 @@ __device__ __forceinline__ void wb_put_full(cpx* row, int mw, const cpx (&v)[16]
       if (m >= 4 && m < 12) continue;
       const int off = (m < 8 ? m : m - 16) * P::NT;
       const int k = t + off;
-      if (k >= -(mw >> 1) && k < (mw >> 1)) buf_st(v[m], r, 8 * t, 8 * (off + P::N / 4));
+      if (k >= -(mw >> 1) && k < (mw >> 1)) buf_st<wct_aux<4>()>(v[m], r, 8 * t, 8 * (off + P::N / 4));
     }
   } else {
 #pragma unroll
@@ -547,7 +571,7 @@ __device__ __forceinline__ void band_load(cpx (&pre)[8], const cpx* __restrict__
       const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(g);
 #pragma unroll
       for (int r = 0; r < B::NZ; ++r)
-        pre[r] = buf_ld_c64(rs, 8 * t, 8 * (r * P::NT + (r < B::NZ / 2 ? B::H : -B::H)));
+        pre[r] = buf_ld_c64<wct_aux<16>()>(rs, 8 * t, 8 * (r * P::NT + (r < B::NZ / 2 ? B::H : -B::H)));
     } else {
 #pragma unroll
       for (int r = 0; r < B::NZ; ++r) pre[r] = g[t + r * P::NT + (r < B::NZ / 2 ? B::H : -B::H)];
@@ -560,7 +584,7 @@ __device__ __forceinline__ void band_load(cpx (&pre)[8], const cpx* __restrict__
     asm volatile("" : "+v"(tt));
     if constexpr (P::NT >= kWave) {  // wave-uniform row: buffer load, lanes t >= M read 0
       const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(g, B::M * static_cast<int>(sizeof(cpx)));
-      pre[0] = buf_ld_c64(rs, tt < B::M ? 8 * ((tt + B::H) & (B::M - 1)) : 8 * B::M, 0);
+      pre[0] = buf_ld_c64<wct_aux<16>()>(rs, tt < B::M ? 8 * ((tt + B::H) & (B::M - 1)) : 8 * B::M, 0);
     } else {
       pre[0] = tt < B::M ? g[(tt + B::H) & (B::M - 1)] : mkc(0.f, 0.f);
     }
@@ -625,10 +649,10 @@ __device__ __forceinline__ void wct_dec_rows(const CwtArgs& a, const WctRowCtx& 
       const bool wr = valid && (c.plan[c.j0 + (valid ? jl : r0)] & kPlanNeedT);
       band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // (T1, T2)
       band_load<LOGN, E>(pre, c.TB + rowbase, t);
-      if (wr) put_row<LOGN, BUF, true>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+      if (wr) put_row<LOGN, BUF, true, wct_aux<2>()>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       band_ifft<LOGN, E, TWL>(v, pre, my, tw, t, par, twl);  // T12
       if (more) band_load<LOGN, E>(pre, dy_row(r + G::ROWS), t);
-      if (wr) put_row<LOGN, BUF, true>(c.TB + rowbase, t, n0, [&](int m) { return v[m]; });
+      if (wr) put_row<LOGN, BUF, true, wct_aux<2>()>(c.TB + rowbase, t, n0, [&](int m) { return v[m]; });
     }
   }
 }
@@ -712,9 +736,9 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       if (pl & kPlanNeedT) {
         const int slot = holder ? k + K0 : -1;
         smooth_from_band<LOGN, 2, TWL>(w1, wy, slot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF, FULL>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+        if (valid) put_row<LOGN, BUF, FULL, wct_aux<2>()>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
         smooth_from_band<LOGN, 2, TWL>(v, zy, slot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF, FULL>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+        if (valid) put_row<LOGN, BUF, FULL, wct_aux<2>()>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       }
       continue;
     }
@@ -747,7 +771,7 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       if (pl_any & kPlanNeedT) {
         fft_row<LOGN, 1, 1, TWL>(v, my, 0, tw, t, par, twl);
         // (T1, T2): smoothed |W1|^2/s, |W2|^2/s
-        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF, FULL>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF, FULL, wct_aux<2>()>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       }
       // the XWT-shaped outputs once z1 is dead (only W12 live: no spills around atan2)
       if (valid) xwt_outputs<LOGN, BUF, FULL>(a, w1, rowbase, t);
@@ -756,7 +780,7 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       if (wb) wb_put_full<LOGN>(wb_row<LOGN>(c.WB, c.b, a.S, c.j0 + jl, 1), mw, w1, t);
       if (pl_any & kPlanNeedT) {
         fft_row<LOGN, 1, 1, TWL>(w1, my, 0, tw, t, par, twl);
-        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF, FULL>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });
+        if (valid && (pl & kPlanNeedT)) put_row<LOGN, BUF, FULL, wct_aux<2>()>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });
       }
     } else {
       int zslot, wslot;
@@ -783,9 +807,9 @@ __device__ __forceinline__ void wct_rows(const CwtArgs& a, const WctRowCtx& c, i
       }
       if (pl_any & kPlanNeedT) {
         smooth_from_band<LOGN, Q, TWL>(w1, wy, wslot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF, FULL>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
+        if (valid) put_row<LOGN, BUF, FULL, wct_aux<2>()>(c.TB + rowbase, t, n0, [&](int m) { return w1[m]; });  // smoothed W12/s
         smooth_from_band<LOGN, Q, TWL>(v, zy, zslot, my, tw, t, par, twl);
-        if (valid) put_row<LOGN, BUF, FULL>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
+        if (valid) put_row<LOGN, BUF, FULL, wct_aux<2>()>(c.TA + rowbase, t, n0, [&](int m) { return v[m]; });
       }
     }
   }
@@ -989,7 +1013,7 @@ __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restric
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       int ix;
-      if (keep(m, ix)) dy[ix] = cscale(v[m], inv_m);
+      if (keep(m, ix)) st_c<64>(dy + ix, cscale(v[m], inv_m));
     }
   }
   // smoothed band: F(k) / (M s); time-path rows -> TA / TB slot in FFT order, band rows -> SB
@@ -1009,9 +1033,9 @@ __device__ __forceinline__ void dec_items(const CwtArgs& a, const cpx* __restric
     const float kk = static_cast<float>(k);
     const cpx y = cscale(v[m], sc * __builtin_amdgcn_exp2f(beta * kk * kk));
     int ix;
-    if (needT && keep(m, ix)) trow[ix] = y;
-    if (needS && k >= -NTN / 2 && k < NTN / 2) sb[k + NTN / 2] = y;
-    if (needW) wb_put(wrow, mw, k, y);
+    if (needT && keep(m, ix)) st_c<64>(trow + ix, y);
+    if (needS && k >= -NTN / 2 && k < NTN / 2) st_c<64>(sb + k + NTN / 2, y);
+    if (needW) wb_put<64>(wrow, mw, k, y);
   }
   if constexpr (M < NTN) {  // band rows' SB bins outside (-M/2, M/2): zero, by the whole workgroup
     constexpr int Z = NTN - M;
@@ -1120,8 +1144,16 @@ static int launch_dec_class(const CwtArgs& a, const cpx* spec, cpx* TA, cpx* TB,
 // one pair (C = 2: 16-byte loads of (T1, T2) and T12 for two columns -- the pass is a
 // pure stream of the workspace); the last K rows of each column stay in registers.
 template <int C> struct ColVec;
-template <> struct ColVec<1> { using T = float2; };
-template <> struct ColVec<2> { using T = float4; };
+template <> struct ColVec<1> { using T = float2; using E = cpx; };
+template <> struct ColVec<2> { using T = float4; using E = f32x4; };
+template <int C>
+__device__ __forceinline__ typename ColVec<C>::T ld_col(const typename ColVec<C>::T* p) {
+  using V = typename ColVec<C>::T;
+  if constexpr (wct_aux<32>() != 0)
+    return __builtin_bit_cast(V, __builtin_nontemporal_load(reinterpret_cast<const typename ColVec<C>::E*>(p)));
+  else
+    return *p;
+}
 
 template <int K, int C, int DD = 0>
 __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, const cpx* __restrict__ TB,
@@ -1159,8 +1191,8 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     if (d < jlim) {
-      pa[d] = cola[static_cast<long long>(d) * ldv];
-      pc[d] = colb[static_cast<long long>(d) * ldv];
+      pa[d] = ld_col<C>(cola + static_cast<long long>(d) * ldv);
+      pc[d] = ld_col<C>(colb + static_cast<long long>(d) * ldv);
     }
   }
   for (int jb = 0; jb < jend; jb += K) {
@@ -1185,8 +1217,8 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
         }
         const int jn = j + D;
         if (jn < jlim) {
-          pa[slot] = cola[static_cast<long long>(jn) * ldv];
-          pc[slot] = colb[static_cast<long long>(jn) * ldv];
+          pa[slot] = ld_col<C>(cola + static_cast<long long>(jn) * ldv);
+          pc[slot] = ld_col<C>(colb + static_cast<long long>(jn) * ldv);
         }
       } else {
 #pragma unroll
@@ -1218,6 +1250,8 @@ __global__ void __launch_bounds__(256) wct_phase_b(const cpx* __restrict__ TA, c
         float* orow = out + static_cast<long long>(i) * n0;
         if constexpr (C == 2)
           *reinterpret_cast<float2*>(orow) = make_float2(o[0], o[1]);
+        else if constexpr (wct_aux<8>() != 0)
+          __builtin_nontemporal_store(o[0], orow);
         else
           orow[0] = o[0];
       }
@@ -1302,8 +1336,8 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
           const bool ok = q < K && rr >= 0 && rr < a.S;
           wq[u] = ok ? ((K > 1 && (q == 0 || q == K - 1)) ? 0.5f * wn : wn) : 0.f;
           const cpx* sb = sbb + (ok ? rr : i) * 2ll * P::NT;
-          lz[u] = sb[0];
-          lw[u] = sb[P::NT];
+          lz[u] = ld_c<256>(sb);
+          lw[u] = ld_c<256>(sb + P::NT);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1322,7 +1356,7 @@ __device__ __forceinline__ void wct_spec_rows(const CwtArgs& a, const cpx* __res
     smooth_from_band_ec<LOGN, EC, TWL, false>(v, yw, slot, my, tw, t, par, twl);
     if (valid) {
       const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
-      put_row<LOGN, BUF, FULL>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
+      put_row<LOGN, BUF, FULL, wct_aux<1>()>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
     }
   }
 }
@@ -1354,8 +1388,8 @@ __global__ void __launch_bounds__(256) wct_wide_boxcar(cpx* __restrict__ WB, lon
     if (j <= jhi) {
       const int mw = N >> plan_ew(plan[j]);
       if (k >= -(mw >> 1) && k < (mw >> 1)) {
-        z = base[(2ll * j) * nb];
-        w = base[(2ll * j + 1) * nb];
+        z = ld_c<128>(base + (2ll * j) * nb);
+        w = ld_c<128>(base + (2ll * j + 1) * nb);
       }
     }
   };
@@ -1391,8 +1425,8 @@ __global__ void __launch_bounds__(256) wct_wide_boxcar(cpx* __restrict__ WB, lon
               sw = cfma(cpx{wq, wq}, rw[slot], sw);
             }
           }
-          base[(2ll * i) * nb] = sz;
-          base[(2ll * i + 1) * nb] = sw;
+          st_c<128>(base + (2ll * i) * nb, sz);
+          st_c<128>(base + (2ll * i + 1) * nb, sw);
         }
       }
     }
@@ -1421,16 +1455,16 @@ __device__ __forceinline__ void wct_wide_rows(const CwtArgs& a, const cpx* __res
     cpx v[16];
     float den[16];
 #pragma unroll
-    for (int q = 0; q < BG::NZ; ++q) pre[q] = zrow[t + q * P::NT];  // shifted bin p -> k = p - H
+    for (int q = 0; q < BG::NZ; ++q) pre[q] = ld_c<256>(zrow + t + q * P::NT);  // shifted bin p -> k = p - H
     band_ifft<LOGN, EU, TWL>(v, pre, my, tw, t, par, twl);
 #pragma unroll
     for (int m = 0; m < 16; ++m) den[m] = v[m].x * v[m].y;  // S1 S2
 #pragma unroll
-    for (int q = 0; q < BG::NZ; ++q) pre[q] = zrow[P::N / 2 + t + q * P::NT];
+    for (int q = 0; q < BG::NZ; ++q) pre[q] = ld_c<256>(zrow + P::N / 2 + t + q * P::NT);
     band_ifft<LOGN, EU, TWL>(v, pre, my, tw, t, par, twl);
     if (valid) {
       const long long rowbase = (b * a.S + i) * static_cast<long long>(a.n0);
-      put_row<LOGN, BUF, FULL>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
+      put_row<LOGN, BUF, FULL, wct_aux<1>()>(coh + rowbase, t, a.n0, [&](int m) { return fast_div(cabs2(v[m]), den[m]); });
     }
   }
 }
