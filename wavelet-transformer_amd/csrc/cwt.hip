@@ -19,6 +19,14 @@
 
 namespace wtmi {
 
+// cache policy of the CWT's output row stores (build knob for A/B runs): sc1 (aux 16), C2
+// 0.775 -> 0.766 ms and C5 203.0 -> 201.4 ms against the default policy; nt (aux 2) was 2-3 %
+// slower (profiles/r05/nt_policy_ab.txt)
+#ifndef WTMI_CWT_ST_AUX
+#define WTMI_CWT_ST_AUX 16
+#endif
+constexpr int kCwtStAux = WTMI_CWT_ST_AUX;
+
 enum : int { kOutW = 1, kOutPow = 2, kOutSig = 4, kOutUV = 8 };
 
 template <int LOGN, int KIND, bool FULL>
@@ -52,17 +60,17 @@ __device__ __forceinline__ void store_row(const cpx (&v)[16], const CwtArgs& a, 
     auto vo = [&](int m, int sz) { return (FULL || tt + m * P::NT < a.n0) ? sz * t : sz * a.n0; };
 #pragma unroll
     for (int m = 0; m < 16; ++m)
-      if constexpr (KIND & kOutW) buf_st(v[m], rw, vo(m, 8), 8 * m * P::NT);
+      if constexpr (KIND & kOutW) buf_st<kCwtStAux>(v[m], rw, vo(m, 8), 8 * m * P::NT);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const float pw = cabs2(v[m]);
       const int o4 = vo(m, 4);
-      if constexpr (KIND & kOutPow) buf_st(pw, rp, o4, 4 * m * P::NT);
-      if constexpr (KIND & kOutSig) buf_st(pw * sg, rs, o4, 4 * m * P::NT);
+      if constexpr (KIND & kOutPow) buf_st<kCwtStAux>(pw, rp, o4, 4 * m * P::NT);
+      if constexpr (KIND & kOutSig) buf_st<kCwtStAux>(pw * sg, rs, o4, 4 * m * P::NT);
       if constexpr (KIND & kOutUV) {
         const float r = sqrtf(pw);
-        buf_st(r > 0.f ? v[m].y / r : 0.f, ru, o4, 4 * m * P::NT);
-        buf_st(r > 0.f ? v[m].x / r : 1.f, rv, o4, 4 * m * P::NT);
+        buf_st<kCwtStAux>(r > 0.f ? v[m].y / r : 0.f, ru, o4, 4 * m * P::NT);
+        buf_st<kCwtStAux>(r > 0.f ? v[m].x / r : 1.f, rv, o4, 4 * m * P::NT);
       }
     }
     return;

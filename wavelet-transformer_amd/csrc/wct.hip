@@ -39,8 +39,11 @@ namespace wtmi {
 #ifndef WTMI_WCT_NT
 #define WTMI_WCT_NT 191
 #endif
+#ifndef WTMI_WCT_AUX
+#define WTMI_WCT_AUX 2
+#endif
 constexpr int kWctNt = WTMI_WCT_NT;
-template <int BIT> constexpr int wct_aux() { return (kWctNt & BIT) ? kNt : 0; }
+template <int BIT> constexpr int wct_aux() { return (kWctNt & BIT) ? WTMI_WCT_AUX : 0; }
 template <int BIT> __device__ __forceinline__ void st_c(cpx* p, cpx v) {
   if constexpr (wct_aux<BIT>() != 0)
     __builtin_nontemporal_store(v, p);
