@@ -304,19 +304,8 @@ __device__ __forceinline__ void fma4(float4& acc, float c, const float4& s) {
 // mapping of syn_level_chain (taps m-L+1 .. m of the thread's chain, M+L-1 LDS reads for
 // M outputs instead of L*M); W_j stores then run along the chain (coalesced for
 // dq >= 64 groups, dq-group runs below: whole 128-byte lines from dq = 8).
-// W_j row stores of the analysis: -1 plain global stores, else buffer stores off the row's
-// wave-uniform descriptor with this cache policy (build knob for A/B runs)
-#ifndef WTMI_MODWT_ST
-#define WTMI_MODWT_ST -1
-#endif
-constexpr int kModwtSt = WTMI_MODWT_ST;
-__device__ __forceinline__ void st_wrow(float4* wrow, __amdgpu_buffer_rsrc_t rs, int q, float4 v) {
-  if constexpr (kModwtSt < 0)
-    wrow[q] = v;
-  else
-    buf_st<(kModwtSt < 0 ? 0 : kModwtSt)>(v, rs, 16 * q, 0);
-}
-
+// (the W_j stores as buffer stores at the default, nt or sc1 policy measured within noise of
+// these plain stores, r05: profiles/r05/nt_policy_ab.txt)
 template <int L, int GROUPS, int T, int CHAIN = 0>
 __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ x, long long ld,
                                                       int n, int level, FilterBank fb,
@@ -341,7 +330,6 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
   for (int j = 1; j <= level; ++j) {
     const int dm = dilation_mod(j, n);
     float4* wrow = reinterpret_cast<float4*>(wout + static_cast<long long>(j - 1) * n);
-    const __amdgpu_buffer_rsrc_t wrs = uniform_rsrc(kModwtSt < 0 ? nullptr : wrow);
     int tl = tid;
     asm volatile("" : "+v"(tl));
     float4 vreg[GROUPS];
@@ -362,7 +350,7 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
             fma4(aw, fb.h[l], vv[m + L - 1 - l]);
             fma4(av, fb.g[l], vv[m + L - 1 - l]);
           }
-          st_wrow(wrow, wrs, q0 + m * dq, aw);
+          wrow[q0 + m * dq] = aw;
           vreg[m] = av;
           pin4(vreg[m]);
         }
@@ -395,7 +383,7 @@ __global__ void __launch_bounds__(T) modwt_vec_kernel(const float* __restrict__ 
           fma4(av, fb.g[l], s);
         }
       }
-      if (tl + k * T < ng) st_wrow(wrow, wrs, q, aw);
+      if (tl + k * T < ng) wrow[q] = aw;
       vreg[k] = av;
       pin4(vreg[k]);
     }
