@@ -529,7 +529,6 @@ __global__ void __launch_bounds__(T, 1)
   const int tid = threadIdx.x;
   const long long b = blockIdx.x;
   const float* win = w + b * static_cast<long long>(level + 1) * n;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool keepV = (keep >> level) & 1ull;
   {
     // all GROUPS loads in flight before the first LDS write (a runtime-trip loop waited on

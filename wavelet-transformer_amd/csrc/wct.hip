@@ -237,7 +237,6 @@ template <int LOGN, int Q, bool TWL, bool PHASOR = true>
 __device__ __forceinline__ void smooth_from_band(cpx (&v)[16], cpx y, int slot, cpx* my, const cpx* tw,
                                                  int t, int& par, const float4* twl) {
   using P = FftPlan<LOGN>;
-  constexpr int K0 = P::N >> (4 * Q + 1);
   constexpr int STEP = P::NT >> (4 * Q);
   __syncthreads();
   if (slot >= 0) my[slot] = y;
