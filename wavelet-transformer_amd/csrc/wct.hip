@@ -35,7 +35,12 @@ namespace wtmi {
 //   1 output rows (power, phase, arrows, phase C coherence), 2 time-path rows T, 4 WB rows,
 //   8 phase B's coherence stores, 16 band_load reads (DY, TA, TB), 32 phase B's reads of T,
 //   64 the decimation kernels' stores (DY, SB, T, WB), 128 the wide boxcar's reads and writes of
-//   WB, 256 phase C's reads of SB and WB
+//   WB, 256 phase C's reads of SB and WB.
+// Default 191 = every class but 64 and 256, measured per class (profiles/r05/nt_policy_ab.txt):
+// C4 3.09 -> 2.98 ms at 512 pairs, 0.452 -> 0.387 ms at 64 (the re-read pair spectra and plan stay
+// cached); 64 and 256 cost the 64-pair shard 7-9 % (those rows are re-read while still cached).
+// WTMI_WCT_AUX: the policy the buffer accesses of the set classes use (2 = nt; sc1 was slower);
+// the pointer accesses (st_c / ld_c, phase B) are nt whenever their class is set.
 #ifndef WTMI_WCT_NT
 #define WTMI_WCT_NT 191
 #endif
