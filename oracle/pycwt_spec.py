@@ -416,32 +416,36 @@ def significance_from_histogram(wlc, outsidecoi, maxscale, significance_level=0.
     """sig95 from the per-scale counters: NaN for scales with points outside the COI, then
     the quantile step for s < maxscale.
 
-    quantile="pycwt" executes pycwt 0.4.0b0's published statements literally (DESIGN 4,
+    quantile="pycwt" (default) executes pycwt 0.4.0b0's published statements (DESIGN 4,
     "Monte-Carlo quantile"):
 
-        wlc = np.ma.zeros([J + 1, nbins])          # never masked: mask is np.ma.nomask
+        wlc = np.ma.zeros([J + 1, nbins])
         ...                                        # wlc[s, int(t)] += 1 per outside-COI point
+        wlc.mask = (wlc.data == 0.)                # after the Monte-Carlo loop: mask empty bins
         R2y = (np.arange(nbins) + 0.5) / nbins
         for s in range(maxscale):
-            sel = ~wlc[s, :].mask                  # ~nomask: the scalar np.True_
-            P = wlc[s, sel].data.cumsum()          # a 0-d boolean index adds an axis: (1, nbins)
+            sel = ~wlc[s, :].mask                  # the scale's non-empty bins
+            P = wlc[s, sel].data.cumsum()
             P = (P - 0.5) / P[-1]
-            sig95[s] = np.interp(significance_level, P, R2y[sel])   # R2y[sel]: (1, nbins)
+            sig95[s] = np.interp(significance_level, P, R2y[sel])
 
-    np.interp needs a 1-D fp, so it raises ValueError("object too deep for desired array")
-    under numpy 1.26.4 (the reference's pin, requirements.txt:25) and 2.x alike
-    (tests/test_wct_sig_host.py runs these lines in both).  quantile="nonempty" is the
-    engine's explicit alternative: interpolation over each scale's non-empty bins (what a
-    masked counter would have selected)."""
-    if quantile not in ("pycwt", "nonempty"):
+    (the mask line is the Python form of Grinsted's wtcsignif.m ``idx=find(ptile~=0)``).
+    quantile="nonempty" is the same rule written on a plain array.  quantile="unmasked" runs
+    the statements without the mask line: the mask is then np.ma.nomask, ``sel`` the scalar
+    True, R2y[sel] has shape (1, nbins) and np.interp raises ValueError("object too deep for
+    desired array") -- r05's reading, kept as an explicit alternative.  Parity unpinned: pycwt
+    is absent from the image (tests/test_wct_sig_host.py runs the lines under numpy 1.26.4)."""
+    if quantile not in ("pycwt", "nonempty", "unmasked"):
         raise ValueError(quantile)
     nbins = wlc.shape[1]
     sig95 = np.zeros(wlc.shape[0])
     sig95[outsidecoi.any(axis=1)] = np.nan
     R2y = (np.arange(nbins) + 0.5) / nbins
-    if quantile == "pycwt":
+    if quantile in ("pycwt", "unmasked"):
         counter = np.ma.zeros(wlc.shape)
         counter[:, :] = wlc
+        if quantile == "pycwt":
+            counter.mask = (counter.data == 0.)
         with np.errstate(invalid="ignore", divide="ignore"):
             for s in range(maxscale):
                 sel = ~counter[s, :].mask
@@ -477,8 +481,8 @@ def pycwt_cache_name(al1, al2, dt, dj, s0, J, wavelet_name="morlet"):
 def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet=None,
                      mc_count=300, rng=None, nbins=1000, noise="pycwt", quantile="pycwt"):
     """pycwt ``wct_significance`` without the disk cache; ``noise`` as in
-    ``rednoise``, ``quantile`` as in ``significance_from_histogram`` (the literal "pycwt"
-    reading raises ValueError after the Monte Carlo whenever maxscale > 0)."""
+    ``rednoise``, ``quantile`` as in ``significance_from_histogram`` (the "unmasked" reading
+    raises ValueError after the Monte Carlo whenever maxscale > 0)."""
     wavelet = wavelet or Morlet(6)
     rng = rng if rng is not None else np.random.default_rng()
     N, sj, outsidecoi, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)

@@ -98,9 +98,8 @@ def gpu_side(args, y, t, y1, y2):
         out["run_wct_no_sig"] = timed(lambda: wct.run_wct(dw, calculate_signficance=False),
                                       args.calls)
     if args.only in (None, "wct", "sig"):
-        # the drop-in's default quantile step raises as pycwt's does; the timed
-        # Monte Carlo is the engine's quantile="nonempty" mode
-        transforms.SIG_QUANTILE = "nonempty"
+        # the drop-in's defaults: pycwt's masked-counter quantile step
+        assert transforms.SIG_QUANTILE == "pycwt"
         out["run_wct_sig_300_passes"] = timed(lambda: wct.run_wct(dw, calculate_signficance=True),
                                               args.sig_calls, warm=1)
         # the significance call's steps, as run_wct performs them
@@ -120,7 +119,7 @@ def gpu_side(args, y, t, y1, y2):
                     lambda: (transforms.ar1(y1)[0], transforms.ar1(y2)[0]))
             st("wct_significance (noise, coherence launches, counter, D2H, quantile)",
                lambda: transforms.wct_significance(a1[0], a1[1], wct.DT, wct.DJ, wct.S0, J,
-                                                   cache=False, seed=11, quantile="nonempty"))
+                                                   cache=False, seed=11))
             geo = st("host geometry (noise length, COI intervals)",
                      lambda: transforms.wct_sig_geometry(wct.DT, wct.DJ, wct.S0, J))
             wlc = np.random.default_rng(0).integers(0, 50, (geo[1].size, 1000)).astype(float)
@@ -158,7 +157,7 @@ def cpu_side(args, y, y1, y2):
         k = args.cpu_sig_passes
         t0 = time.perf_counter()
         pc.wct_significance(a1, a2, 1 / 12, 1 / 8, 2 / 12, J, mc_count=k,
-                            rng=np.random.default_rng(1), quantile="nonempty")
+                            rng=np.random.default_rng(1))
         per_pass = (time.perf_counter() - t0) / k
         nosig = out.get("run_wct_no_sig", {}).get("median_ms")
         out["run_wct_sig_300_passes"] = {

@@ -112,8 +112,7 @@ def test_wct_significance_long_noise():
     J = int(np.round(np.log2(n0 * DT / s0) / dj))
     N, sj, _, _, anyout, maxscale = transforms.wct_sig_geometry(DT, dj, s0, J)
     assert N > 16384
-    sig = transforms.wct_significance(0.6, 0.4, DT, dj, s0, J, mc_count=60, cache=False, seed=3,
-                                      quantile="nonempty")
+    sig = transforms.wct_significance(0.6, 0.4, DT, dj, s0, J, mc_count=60, cache=False, seed=3)
     assert sig.shape == (J + 1,)
     ok = sig[:maxscale]
     assert np.isfinite(ok).all() and (ok > 0).all() and (ok <= 1).all()

@@ -80,10 +80,6 @@ def test_plot_xwt_and_wct_on_sample_pair(monkeypatch):
     _render(fig)
 
     dw = wct.DataForWCT(y1, y2, wct.MOTHER_DICT[wct.MOTHER], wct.DT, wct.DJ, wct.S0, wct.LEVELS)
-    from wtmi import transforms
-    with pytest.raises(ValueError, match="object too deep"):  # pycwt's quantile step
-        wct.run_wct(dw, calculate_signficance=True, significance_level=0.95)
-    monkeypatch.setattr(transforms, "SIG_QUANTILE", "nonempty")
     rw = wct.run_wct(dw, calculate_signficance=True, significance_level=0.95)
     fig, ax = plt.subplots(1, 1, figsize=(10, 8))
     wct.plot_wct(ax, dw, rw, include_significance=True, include_cone_of_influence=True,

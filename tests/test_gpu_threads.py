@@ -46,7 +46,7 @@ def _jobs(ys, y2):
         g1, g2 = transforms.ar1(ys[i])[0], transforms.ar1(y2[i])[0]
         J = int(np.round(np.log2(ys[i].size * wct.DT / wct.S0) / wct.DJ))
         sig = transforms.wct_significance(g1, g2, wct.DT, wct.DJ, wct.S0, J, mc_count=40,
-                                          cache=False, seed=1234 + i, quantile="nonempty")
+                                          cache=False, seed=1234 + i)
         return [r.coherence, r.phase_diff_u, r.phase_diff_v, sig]
 
     def job_modwt(i):

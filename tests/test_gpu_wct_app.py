@@ -226,18 +226,18 @@ def test_src_xwt_and_wct(monkeypatch):
     refw = gs.run_wct(y1, y2, wct.DT, wct.DJ, wct.S0)
     gate("run_wct coherence abs", np.abs(rw.coherence - refw[0]), 1e-4)
     assert np.isinf(rw.significance_levels).all() and np.isinf(refw[2]).all()  # quirk B.8
-    # significance on: pycwt's quantile step raises ("Monte-Carlo quantile"), so
-    # does the drop-in by default; quantile="nonempty" gives Monte-Carlo levels
-    # (test_gpu_wct_sig.py pins them statistically), the coherence unchanged and the ratio
-    # |coh| / sig95 per scale
+    # significance on (the reference's default): Monte-Carlo levels from pycwt's masked
+    # counter ("Monte-Carlo quantile"; test_gpu_wct_sig.py pins them statistically),
+    # the coherence unchanged and the ratio |coh| / sig95 per scale; the explicit
+    # quantile="unmasked" reading raises
     from wtmi import transforms
-    with pytest.raises(ValueError, match="object too deep for desired array"):
-        wct.run_wct(dw, calculate_signficance=True)
-    monkeypatch.setattr(transforms, "SIG_QUANTILE", "nonempty")
     rs = wct.run_wct(dw, calculate_signficance=True)
     np.testing.assert_array_equal(rs.coherence, rw.coherence)
     fin = np.isfinite(rs.significance_levels)
     assert fin.any() and (rs.significance_levels[fin] > 0).all()
+    monkeypatch.setattr(transforms, "SIG_QUANTILE", "unmasked")
+    with pytest.raises(ValueError, match="object too deep for desired array"):
+        wct.run_wct(dw, calculate_signficance=True)
 
 
 @pytest.mark.parametrize("normalize", [True, False])

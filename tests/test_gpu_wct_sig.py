@@ -83,10 +83,8 @@ def test_coherence_histogram_exact(B, S, n0, nh):
 def test_wct_significance_matches_oracle_monte_carlo(noise):
     from wtmi import transforms
     args = (0.5, 0.3, 1.0, 0.25, 2.0, 12)
-    got = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=False, noise=noise,
-                                      quantile="nonempty")
-    refs = np.array([pc.wct_significance(*args, mc_count=300, rng=np.random.default_rng(i), noise=noise,
-                                         quantile="nonempty")
+    got = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=False, noise=noise)
+    refs = np.array([pc.wct_significance(*args, mc_count=300, rng=np.random.default_rng(i), noise=noise)
                      for i in range(3)])
     ref = refs.mean(axis=0)
     np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
@@ -95,11 +93,9 @@ def test_wct_significance_matches_oracle_monte_carlo(noise):
     assert d.max() < 0.06, (got, ref)
     assert d.mean() < 0.025, (got, ref)
     # reproducible for a fixed seed, and cached per argument set (the noise mode is in the key)
-    again = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True, noise=noise,
-                                        quantile="nonempty")
+    again = transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True, noise=noise)
     np.testing.assert_array_equal(again, got)
-    assert transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True, noise=noise,
-                                      quantile="nonempty") is not again
+    assert transforms.wct_significance(*args, mc_count=300, seed=2024, cache=True, noise=noise) is not again
 
 
 def test_wct_significance_noise_modes_and_g0_raises():
@@ -110,9 +106,8 @@ def test_wct_significance_noise_modes_and_g0_raises():
     literal (white) reading; g == 0 raises AttributeError as pycwt's rednoise does (np.randn)."""
     from wtmi import transforms
     args = (0.98, 0.98, 1 / 12, 1 / 8, 2 / 12, 56)
-    white = transforms.wct_significance(*args, mc_count=100, seed=5, cache=False, quantile="nonempty")
-    red = transforms.wct_significance(*args, mc_count=100, seed=5, cache=False, noise="red",
-                                     quantile="nonempty")
+    white = transforms.wct_significance(*args, mc_count=100, seed=5, cache=False)
+    red = transforms.wct_significance(*args, mc_count=100, seed=5, cache=False, noise="red")
     ok = np.isfinite(white) & np.isfinite(red)
     np.testing.assert_array_equal(ok, np.isfinite(white))
     assert ok.sum() > 10
@@ -132,21 +127,21 @@ def test_run_wct_with_significance_app_shape(monkeypatch):
     y1 = red_series(rng, n, a=0.5).astype(np.float64)  # stationary: pycwt's ar1 has a bound
     y2 = 0.5 * y1 + red_series(rng, n, a=0.3)
     d = wct.DataForWCT(y1, y2, Morlet(6), 1 / 12, 1 / 8, 2 / 12, wct.WCT_LEVELS)
-    with pytest.raises(ValueError, match="object too deep for desired array"):
-        wct.run_wct(d, calculate_signficance=True)  # pycwt's quantile step (the default)
-    from wtmi import transforms
-    monkeypatch.setattr(transforms, "SIG_QUANTILE", "nonempty")
-    res = wct.run_wct(d, calculate_signficance=True)
+    res = wct.run_wct(d, calculate_signficance=True)  # the reference's default
     assert res.significance_levels.shape == res.coherence.shape
     fin = np.isfinite(res.significance_levels)
     assert fin.mean() > 0.5  # NaN only on the scales pycwt leaves NaN
     assert (res.significance_levels[fin] > 0).all()
+    from wtmi import transforms
+    monkeypatch.setattr(transforms, "SIG_QUANTILE", "unmasked")  # the explicit raising reading
+    with pytest.raises(ValueError, match="object too deep for desired array"):
+        wct.run_wct(d, calculate_signficance=True)
 
 
-def test_run_wct_significance_matches_oracle_in_pycwt_mode(monkeypatch):
+def test_run_wct_significance_matches_oracle_with_defaults(monkeypatch):
     """The drop-in run_wct(calculate_signficance=True) end to end -- ar1 of the raw series,
-    pycwt's literal (white) noise, 300 passes, the ratio |WCT| / sig95 -- against the oracle's
-    pycwt.wct_significance in the same mode: the levels the ratio implies per scale agree
+    pycwt's literal (white) noise, 300 passes, pycwt's masked-counter quantile, the ratio
+    |WCT| / sig95 -- against the oracle's pycwt.wct_significance with its defaults: the levels the ratio implies per scale agree
     with the mean of 3 oracle seeds within 0.06 (mean 0.02); 5 oracle seeds of this geometry
     spread by at most 0.031 (mean 0.0075) around that mean."""
     import src.wct as wct
@@ -157,15 +152,12 @@ def test_run_wct_significance_matches_oracle_in_pycwt_mode(monkeypatch):
     y1 = red_series(rng, n, a=0.5).astype(np.float64)
     y2 = 0.5 * y1 + red_series(rng, n, a=0.3)
     d = wct.DataForWCT(y1, y2, Morlet(6), dt, dj, s0, wct.WCT_LEVELS)
-    from wtmi import transforms
-    monkeypatch.setattr(transforms, "SIG_QUANTILE", "nonempty")
     res = wct.run_wct(d, calculate_signficance=True)
     with np.errstate(divide="ignore", invalid="ignore"):
         implied = np.nanmedian(np.abs(res.coherence) / res.significance_levels, axis=1)
     a1, a2 = pc.ar1(y1)[0], pc.ar1(y2)[0]
     J = res.coherence.shape[0] - 1
-    ref = np.mean([pc.wct_significance(a1, a2, dt, dj, s0, J, mc_count=300, rng=np.random.default_rng(i),
-                                       quantile="nonempty")
+    ref = np.mean([pc.wct_significance(a1, a2, dt, dj, s0, J, mc_count=300, rng=np.random.default_rng(i))
                    for i in range(3)], axis=0)
     ok = np.isfinite(ref)
     np.testing.assert_array_equal(np.isfinite(implied), ok)

@@ -79,19 +79,19 @@ def test_oracle_rednoise_modes():
 
 def test_quantile_known_answer_with_empty_bins_at_the_crossing():
     """Hand-built counter: 10 counts in bin 0, bins 1-4 EMPTY, 10 counts in bin 5 (nbins 10).
-    The "nonempty" rule (the engine's explicit alternative) interpolates over non-empty bins only: P = ((10, 20) - 0.5) / 20 =
+    The "nonempty" rule (pycwt's masked counter, the default) interpolates over non-empty bins only: P = ((10, 20) - 0.5) / 20 =
     (0.475, 0.975) on the mid-bin grid (0.05, 0.55), so the 95 % level is
-    0.05 + (0.95 - 0.475) / 0.5 * 0.5 = 0.525.  (Parity unpinned: pycwt's own quantile step
-    raises, test_pycwt_quantile_statements_raise; no reference fixture exists for this step.)"""
+    0.05 + (0.95 - 0.475) / 0.5 * 0.5 = 0.525 -- also what pycwt's masked counter selects
+    (quantile="pycwt").  (Parity unpinned: no reference fixture exists for this step.)"""
     from wtmi import transforms
     wlc = np.zeros((2, 10))
     wlc[0, 0] = wlc[0, 5] = 10
     got = transforms.significance_from_histogram(wlc, np.array([True, True]), 1, 0.95)
     assert got[0] == pytest.approx(0.525, abs=1e-15)
     assert np.isnan(got[1])
-    ref = pc.significance_from_histogram(wlc, np.ones((2, 4), dtype=bool), 1, 0.95,
-                                         quantile="nonempty")
-    assert ref[0] == pytest.approx(0.525, abs=1e-15)
+    for q in ("nonempty", "pycwt"):
+        ref = pc.significance_from_histogram(wlc, np.ones((2, 4), dtype=bool), 1, 0.95, quantile=q)
+        assert ref[0] == pytest.approx(0.525, abs=1e-15)
 
 
 def test_significance_cache_persists_on_disk(tmp_path, monkeypatch):
@@ -116,9 +116,11 @@ def test_significance_cache_persists_on_disk(tmp_path, monkeypatch):
 
 
 # pycwt 0.4.0b0 wavelet.wct_significance, the counter and the quantile step as published
-# (the loop body over Monte-Carlo passes replaced by fixed counts).  Executed as written, in
+# (the loop body over Monte-Carlo passes replaced by fixed counts; MASK_LINE is the line
+# ``wlc.mask = (wlc.data == 0.)`` that follows the Monte-Carlo loop).  Executed as written, in
 # this interpreter and under the reference's numpy pin (requirements.txt:25, numpy 1.26.4).
 PYCWT_QUANTILE_LINES = """
+import json
 import numpy as np
 J, nbins, maxscale, significance_level = 5, 1000, 4, 0.95
 sig95 = np.zeros(J + 1)
@@ -127,6 +129,8 @@ rng = np.random.default_rng(0)
 for s in range(maxscale):
     for t in np.floor(rng.beta(2, 5, 400) * nbins):
         wlc[s, int(t)] += 1
+counts = wlc.data.tolist()
+MASK_LINE
 R2y = (np.arange(nbins) + 0.5) / nbins
 try:
     for s in range(maxscale):
@@ -134,54 +138,87 @@ try:
         P = wlc[s, sel].data.cumsum()
         P = (P - 0.5) / P[-1]
         sig95[s] = np.interp(significance_level, P, R2y[sel])
-    print("RESULT ok", np.__version__, sig95[:maxscale].tolist())
+    print("RESULT ok", np.__version__, json.dumps({"sig95": sig95[:maxscale].tolist(), "wlc": counts}))
 except Exception as e:
     print("RESULT", type(e).__name__, np.__version__, sel.shape, R2y[sel].shape, e)
 """
 PY39 = "/opt/conda/bin/python3.9"
 
 
-def _run_quantile_lines(cmd):
-    out = subprocess.run(cmd, input=PYCWT_QUANTILE_LINES, capture_output=True, text=True,
+def _run_quantile_lines(cmd, masked=True):
+    src = PYCWT_QUANTILE_LINES.replace("MASK_LINE", "wlc.mask = (wlc.data == 0.)" if masked else "")
+    out = subprocess.run(cmd, input=src, capture_output=True, text=True,
                          timeout=120, env={**os.environ, "PYTHONWARNINGS": "ignore"})
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("RESULT")]
     assert line, out.stdout + out.stderr
-    print(line[-1])
+    print(line[-1][:200])
     return line[-1]
 
 
-def test_pycwt_quantile_statements_raise():
-    """pycwt's counter is np.ma.zeros and is never masked, so ``~wlc[s, :].mask`` is the scalar
-    True, a 0-d boolean index adds an axis (R2y[sel] has shape (1, nbins)) and np.interp
-    raises ValueError('object too deep for desired array') -- under numpy 1.26.4 (the
-    reference's pin; /opt/conda/bin/python3.9 when present) and this interpreter's numpy.
-    The oracle's quantile="pycwt" runs the same statements; the engine's default raises the
-    same error before any GPU work ("Monte-Carlo quantile")."""
+def _interpreters():
     import sys
-    here = _run_quantile_lines([sys.executable, "-"])
-    assert here.startswith("RESULT ValueError") and "object too deep for desired array" in here
-    assert "(1, 1000)" in here
+    yield sys.executable, None
     if os.path.exists(PY39):
-        pinned = _run_quantile_lines([PY39, "-"])
-        assert pinned.startswith("RESULT ValueError 1.26.4"), pinned
-        assert "object too deep for desired array" in pinned
-    # the oracle's literal reading: the same failure on any counter with maxscale > 0
+        yield PY39, "1.26.4"
+
+
+@pytest.mark.parametrize("cmd,version", list(_interpreters()))
+def test_pycwt_quantile_statements_equal_the_nonempty_rule(cmd, version):
+    """pycwt's quantile step as published -- the np.ma counter masked at its empty bins after the
+    Monte Carlo, then np.interp over each scale's unmasked bins -- run as written, under this
+    interpreter's numpy and under numpy 1.26.4 (the reference's pin, /opt/conda/bin/python3.9
+    when present), returns EXACTLY what the oracle's "nonempty" rule, the engine's host rule and
+    (tests/test_gpu_wct_sig.py) its device kernel K15 return on the same counters."""
+    import json
+    from wtmi import transforms
+    line = _run_quantile_lines([cmd, "-"], masked=True)
+    assert line.startswith("RESULT ok"), line
+    if version is not None:
+        assert line.split()[2] == version
+    res = json.loads(line.split(" ", 3)[3])
+    wlc = np.asarray(res["wlc"])
+    literal = np.asarray(res["sig95"])
+    outside = np.ones((wlc.shape[0], 4), bool)
+    ref = pc.significance_from_histogram(wlc, outside, 4, 0.95, quantile="nonempty")
+    np.testing.assert_array_equal(literal, ref[:4])
+    np.testing.assert_array_equal(pc.significance_from_histogram(wlc, outside, 4, 0.95), ref)
+    eng = transforms.significance_from_histogram(wlc, outside.any(axis=1), 4, 0.95)
+    np.testing.assert_allclose(eng[:4], literal, rtol=0, atol=1e-15)
+
+
+def test_unmasked_quantile_reading_raises():
+    """Without the mask line the counter's mask is np.ma.nomask, ``~wlc[s, :].mask`` is the
+    scalar True, a 0-d boolean index adds an axis (R2y[sel] has shape (1, nbins)) and np.interp
+    raises ValueError('object too deep for desired array') under numpy 1.26.4 and 2.x.  That
+    reading (r05's default) is kept only as the explicit quantile="unmasked" option."""
+    for cmd, version in _interpreters():
+        here = _run_quantile_lines([cmd, "-"], masked=False)
+        assert here.startswith("RESULT ValueError") and "object too deep for desired array" in here
+        assert "(1, 1000)" in here
+        if version is not None:
+            assert here.startswith(f"RESULT ValueError {version}"), here
     wlc = np.zeros((3, 1000))
     wlc[:2, 100:900] = 1
     with pytest.raises(ValueError, match="object too deep"):
-        pc.significance_from_histogram(wlc, np.ones((3, 4), bool), 2, 0.95)
+        pc.significance_from_histogram(wlc, np.ones((3, 4), bool), 2, 0.95, quantile="unmasked")
     with pytest.raises(ValueError, match="object too deep"):
-        pc.wct_significance(0.5, 0.3, 1.0, 0.5, 2.0, 4, mc_count=2, rng=np.random.default_rng(0))
+        pc.wct_significance(0.5, 0.3, 1.0, 0.5, 2.0, 4, mc_count=2, rng=np.random.default_rng(0),
+                            quantile="unmasked")
+    # the default (masked) reading returns levels on the same inputs
+    got = pc.wct_significance(0.5, 0.3, 1.0, 0.5, 2.0, 4, mc_count=2, rng=np.random.default_rng(0))
+    assert np.isfinite(got[:2]).all()
     # maxscale == 0: the loop never runs, pycwt returns its initial levels
-    got = pc.significance_from_histogram(wlc, np.zeros((3, 4), bool), 0, 0.95)
+    got = pc.significance_from_histogram(wlc, np.zeros((3, 4), bool), 0, 0.95, quantile="unmasked")
     np.testing.assert_array_equal(got, np.zeros(3))
 
 
-def test_engine_quantile_default_is_pycwt_and_raises_before_gpu_work():
+def test_engine_quantile_default_is_pycwt_masked_and_unmasked_raises_before_gpu_work():
     from wtmi import transforms
-    assert transforms.SIG_QUANTILE == "pycwt" and transforms.QUANTILE_MODES == ("pycwt", "nonempty")
+    assert transforms.SIG_QUANTILE == "pycwt"
+    assert transforms.QUANTILE_MODES == ("pycwt", "nonempty", "unmasked")
     with pytest.raises(ValueError, match="object too deep for desired array"):
-        transforms.wct_significance(0.7, 0.5, 1 / 12, 1 / 8, 2 / 12, 56, cache=False)
+        transforms.wct_significance(0.7, 0.5, 1 / 12, 1 / 8, 2 / 12, 56, cache=False,
+                                    quantile="unmasked")
     with pytest.raises(ValueError, match="quantile must be one of"):
         transforms.wct_significance(0.7, 0.5, 1 / 12, 1 / 8, 2 / 12, 56, quantile="median")
     # g == 0 fails first (pycwt's rednoise runs in the Monte-Carlo loop, before the quantile)
@@ -192,8 +229,7 @@ def test_engine_quantile_default_is_pycwt_and_raises_before_gpu_work():
 def test_pycwt_cache_name_is_nan_above_a_quarter():
     """pycwt's cache file name rounds arctanh(4 al): NaN for |al| > 0.25, so every such pair of
     series shares one name per (dj, s0 / dt, J, wavelet).  The engine keys on the exact al
-    (its cache is only filled in the quantile="nonempty" mode; pycwt's literal quantile step
-    raises before its cache write, so pycwt never writes such a file either)."""
+    and does not reproduce the sharing, which would hand one series' levels to another."""
     a = pc.pycwt_cache_name(0.98, 0.6, 1 / 12, 1 / 8, 2 / 12, 75)
     b = pc.pycwt_cache_name(0.3, 0.9, 1 / 12, 1 / 8, 2 / 12, 75)
     assert a == b == "wct_sig_nan_nan_0.12500_2.00000_75_morlet"

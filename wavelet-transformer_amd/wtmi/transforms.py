@@ -440,12 +440,16 @@ def sig_cache_store(key, sig95) -> None:
 SIG_NOISE = os.environ.get("WTMI_SIG_NOISE", "pycwt")
 
 # Quantile step of wct_significance ("Monte-Carlo quantile"; parity unpinned):
-# "pycwt" (default) behaves as pycwt 0.4.0b0's published lines do -- its counter is
-# np.ma.zeros (never masked), so ``sel = ~wlc[s, :].mask`` is the scalar True, R2y[sel] is
-# 2-D and np.interp raises ValueError("object too deep for desired array") under numpy 1.26.4
-# (the reference's pin) and 2.x; "nonempty" is the engine's alternative: the levels
-# interpolated over each scale's non-empty bins (ops.coherence_quantile).
-QUANTILE_MODES = ("pycwt", "nonempty")
+# "pycwt" (default) is pycwt 0.4.0b0's published step: after the Monte-Carlo passes it masks
+# the empty bins of its np.ma counter (``wlc.mask = (wlc.data == 0.)``) and, per scale,
+# np.interp's the level over the non-empty bins (P = (cumsum - 0.5) / total on the mid-bin grid)
+# -- ops.coherence_quantile on the device.  "nonempty" is the same rule under its r01-r05 name.
+# "unmasked" is the explicit alternative reading without that mask line (the counter's mask is
+# np.ma.nomask, ``~wlc[s, :].mask`` the scalar True, R2y[sel] 2-D): np.interp raises
+# ValueError("object too deep for desired array") -- what r05 made the default.  The reference's
+# own script (src/wct.py:453-465) and the app's significance checkbox (app/ui.py:74-81 ->
+# src/wavelet_plots.py:510-514) plot levels from this call, so the masked reading is the default.
+QUANTILE_MODES = ("pycwt", "nonempty", "unmasked")
 SIG_QUANTILE = os.environ.get("WTMI_SIG_QUANTILE", "pycwt")
 PYCWT_QUANTILE_ERROR = "object too deep for desired array"
 
@@ -461,10 +465,12 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
     under the user cache dir (src/wct.py:117); ``seed`` None draws a fresh one, as pycwt's
     unseeded draws do.  Like pycwt's rednoise (whose g == 0 branch calls the nonexistent
     ``np.randn``), a zero lag-1 coefficient raises AttributeError in the "pycwt" mode.
-    ``quantile`` ("pycwt" or "nonempty", default ``SIG_QUANTILE``): in the "pycwt" mode the
-    call raises ValueError as pycwt's quantile step does once maxscale > 0 (pycwt raises it
-    after its mc_count passes and before it writes its cache; the passes change nothing
-    observable, so they are not run)."""
+    ``quantile`` (``QUANTILE_MODES``, default ``SIG_QUANTILE`` = "pycwt"): "pycwt" and its
+    alias "nonempty" interpolate each scale's level over its non-empty bins, as pycwt's masked
+    counter selects them; "unmasked" raises ValueError once maxscale > 0, as pycwt's step would
+    without its mask line (it would raise after the passes, which change nothing observable,
+    so they are not run).  Cache order: pycwt reads its cache file before the Monte Carlo, and
+    so does this call (a hit returns before any launch)."""
     wavelet = as_morlet(wavelet)
     if wavelet.deltaj0 <= 0:
         raise ValueError("wct_significance needs a Morlet(6) wavelet (deltaj0 defined)")
@@ -478,10 +484,12 @@ def wct_significance(al1, al2, dt, dj, s0, J, significance_level=0.95, wavelet="
         raise AttributeError("module 'numpy' has no attribute 'randn' "
                              "(pycwt helpers.rednoise with g == 0)")
     N, sj, t_lo, t_hi, anyout, maxscale = wct_sig_geometry(dt, dj, s0, J, wavelet)
-    if quantile == "pycwt" and maxscale > 0:
-        raise ValueError(f"{PYCWT_QUANTILE_ERROR} (pycwt 0.4.0b0 wct_significance: np.interp "
-                         "over the unmasked np.ma counter; quantile='nonempty' or "
-                         "WTMI_SIG_QUANTILE=nonempty gives the levels)")
+    if quantile == "nonempty":
+        quantile = "pycwt"  # one rule, one cache entry
+    if quantile == "unmasked" and maxscale > 0:
+        raise ValueError(f"{PYCWT_QUANTILE_ERROR} (quantile='unmasked': np.interp over the "
+                         "np.ma counter without pycwt's wlc.mask = (wlc.data == 0.); the "
+                         "default quantile='pycwt' gives the levels)")
     # the key holds the exact lag-1 coefficients (pycwt's cache name rounds arctanh(4 al),
     # NaN for |al| > 0.25)
     cache = cache and SIG_CACHE
