@@ -466,7 +466,10 @@ def step_bound(cfg, per_step, step_ms, hbm_frac):
     holding every kernel of the step: "hbm" and no VALU fraction."""
     import glob
     out = {"bound": "hbm", "hbm": hbm_frac, "valu": None, "valu_insts_per_step": None,
-           "source": None}
+           "source": None,
+           "note": "valu = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz x step time): a model; "
+                   "transcendental ops issue at a quarter rate (undercounted) and packed FP32 ops do "
+                   "two lanes' work (overcounted relative to scalar), so read it to about +-20 %"}
     if not per_step or not step_ms:
         return out
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_roofline.json")), reverse=True):

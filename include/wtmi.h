@@ -97,8 +97,9 @@ int wtmi_wct_morlet(const float* x1, const float* x2, long long ld, long long ba
                     float* out_v, void* stream);
 
 /* Side-stream pool entries the full-row WCT (n0 = 2^k >= 1024) has created in this process:
- * a call takes ONE entry (two streams: the full-band rows' chain and, for batches of at most
- * 256 pairs, phase C's q windows) from a per-device pool and joins both before returning
+ * a call takes ONE entry (two streams and five events, created together: the full-band rows'
+ * chain and, when wct_pc_early selects it -- by default for batches of at most 256 pairs --
+ * phase C's q windows) from a per-device pool and joins both before returning
  * (on error paths too), so the count is the most such calls that ever overlapped, not the
  * number of host threads that made one.                                             */
 long long wtmi_wct_side_streams(void);

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build a variant of libwtmi.so with extra compile flags (for scripts/ab_bench.sh A/B runs):
-#   bash scripts/debug/build_variant.sh NAME "-DWTMI_ST_AUX=2 ..."
+#   bash scripts/debug/build_variant.sh NAME "-DWTMI_CWT_ST_AUX=0 -DWTMI_WCT_NT=0 -DWTMI_WCT_AUX=2"
+# (the build knobs the sources read: WTMI_CWT_ST_AUX in cwt.hip, WTMI_WCT_NT / WTMI_WCT_AUX in wct.hip)
 # -> scripts/_var/NAME/libwtmi.so (git-ignored; travels to the GPU box with the tree).
 set -eu
 name=$1; extra=$2

@@ -145,7 +145,13 @@ def test_roofline_bound_follows_the_committed_profile(cfg, bound):
         line = json.load(fh)
     hbm = line["roofline"]["achieved"] / line["roofline"]["peak"]
     sb = bench.step_bound(cfg, bench.CONFIGS[cfg].PER_STEP, line["roofline"]["kernel_ms"], hbm)
-    assert sb["bound"] == bound, sb
     assert sb["source"] and 0 < sb["valu"] < 1 and sb["hbm"] == hbm
+    # the VALU fraction is a model (every VALU instruction at 4 cycles per wave64: transcendental
+    # ops issue slower, packed FP32 does two lanes' work), so the ordering is checked with a
+    # margin rather than the label alone: the binding resource is ahead by at least 1.25x
+    hi, lo = (sb["valu"], hbm) if bound == "valu" else (hbm, sb["valu"])
+    assert hi > 1.25 * lo, sb
+    assert sb["bound"] == bound, sb
+    assert "note" in sb
     if "step_fractions" in line["roofline"]:  # lines written since the field exists
         assert line["roofline"]["bound"] == bound

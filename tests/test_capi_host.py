@@ -211,3 +211,24 @@ def test_launch_options_are_thread_local():
     assert mine != default
     assert seen["other"] == default
     assert _lib.get_option("cwt_prune") == default
+
+
+def test_out_of_range_environment_option_warns_and_keeps_default():
+    """WTMI_<NAME> outside the option's range (or not an integer) is not applied, and says so
+    on stderr: an A/B run with a mistyped knob must not silently measure the default."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from wtmi import _lib; "
+            "print('VAL', _lib.get_option('modwt_syn'), _lib.get_option('wct_depth'), "
+            "_lib.get_option('wct_wide'))" % os.path.join(ROOT, "wavelet-transformer_amd"))
+    env = {**os.environ, "WTMI_MODWT_SYN": "5", "WTMI_WCT_DEPTH": "0", "WTMI_WCT_WIDE": "x"}
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                         env=env)
+    assert out.returncode == 0, out.stderr
+    from wtmi import _lib
+    default_syn, default_wide = _lib.get_option("modwt_syn"), _lib.get_option("wct_wide")
+    if "WTMI_MODWT_SYN" not in os.environ and "WTMI_WCT_WIDE" not in os.environ:
+        assert f"VAL {default_syn} 0 {default_wide}" in out.stdout, out.stdout
+    assert "ignoring WTMI_MODWT_SYN=5 (expected an integer in [0, 2])" in out.stderr, out.stderr
+    assert "ignoring WTMI_WCT_WIDE=x" in out.stderr, out.stderr
+    assert "WTMI_WCT_DEPTH" not in out.stderr

@@ -240,7 +240,8 @@ def test_wct_launch_policies_bitwise_equal(n0, B):
     ref = run()
     for opts in ({"wct_dec_merge": 0}, {"wct_dec_merge": 1}, {"wct_side_stream": 0},
                  {"wct_pc_early": 0}, {"wct_pc_early": 1}, {"wct_min_rows": 1},
-                 {"wct_dec_merge": 1, "wct_min_rows": 2, "wct_dec_rows": 2}):
+                 {"wct_dec_merge": 1, "wct_min_rows": 2, "wct_dec_rows": 2},
+                 {"wct_depth": 0}, {"wct_depth": 0, "wct_pc_early": 1}):
         ctx = [_lib.option(k, v) for k, v in opts.items()]
         for c in ctx:
             c.__enter__()

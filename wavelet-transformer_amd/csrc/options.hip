@@ -1,4 +1,5 @@
 // Launch-policy options (common.hpp Options): environment read once, C ABI setter.
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -38,8 +39,15 @@ const Options& env_options() {
       for (const char* c = e.name; *c && k + 1 < sizeof(env); ++c) env[k++] = static_cast<char>(*c >= 'a' && *c <= 'z' ? *c - 32 : *c);
       env[k] = 0;
       if (const char* v = getenv(env)) {
-        const long x = strtol(v, nullptr, 10);
-        if (x >= e.lo && x <= e.hi) o.*(e.field) = static_cast<int>(x);
+        char* end = nullptr;
+        const long x = strtol(v, &end, 10);
+        if (end != v && *end == 0 && x >= e.lo && x <= e.hi) {
+          o.*(e.field) = static_cast<int>(x);
+        } else {
+          // an ignored knob must not pass silently (an A/B would measure the default)
+          fprintf(stderr, "wtmi: ignoring %s=%s (expected an integer in [%d, %d]); keeping %d\n", env, v,
+                  e.lo, e.hi, o.*(e.field));
+        }
       }
     }
     return o;
