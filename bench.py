@@ -211,6 +211,11 @@ class Workload:
         self.local = self.hi - self.lo
         self.setup()
 
+    def outputs(self):
+        """What this rank's step leaves in HBM for a consumer: the device tensors the host
+        gather copies back, and a note saying what they are."""
+        return [], "none"
+
     def shard_config(self, world, scaling):
         return {"global_batch": self.global_batch, "per_rank_batch": self.local,
                 "rank0_rows": [self.lo, self.hi], "scaling": scaling,
@@ -246,6 +251,9 @@ class C2(Workload):
         ref = pc.cwt(x.astype(np.float64), DT, self.dj, 2 * DT, self.J)[0]
         return float((np.linalg.norm(W.astype(np.complex128) - ref, axis=1)
                       / np.linalg.norm(ref, axis=1)).max())
+
+    def outputs(self):
+        return [self.out], "complex64 W [series, scales, samples]"
 
     def check(self):
         """First and last series of this rank's output vs the oracle (max row error)."""
@@ -290,6 +298,19 @@ class C5(C2):
             e = min(self.local, c + self.chunk)
             self.ops.cwt_morlet(self.x[c:e], self.sjd, DT, 6.0, out_w=self.out[:e - c])
 
+    def outputs(self):
+        """C5's W is never resident (1.1 PB): what a consumer takes home is a checksum per
+        series of the chunk in the buffer (sum of |W|^2 over scales and samples, fp64) plus
+        the sampled parity subset -- the chunk's first, middle and last series' whole W."""
+        torch = self.torch
+        n = min(self.chunk, self.local)
+        if n == 0:
+            return [], "none"
+        chk = self.out[:n].abs().square().sum(dim=(1, 2), dtype=torch.float64)
+        rows = sorted({0, n // 2, n - 1})
+        return [chk, self.out[rows]], ("per-series checksums (f64) of the last chunk + the W rows "
+                                       "of its series %s" % rows)
+
     def check(self):
         """The last chunk's first and last series (the buffer holds the last chunk)."""
         c0 = (self.local - 1) // self.chunk * self.chunk
@@ -327,6 +348,10 @@ class C3(Workload):
         if self.local:
             w = self.ops.modwt(self.x, self.w.dec_lo, self.w.dec_hi, self.J)
             self.xr = self.ops.imodwt(w, self.w.dec_lo, self.w.dec_hi)
+            self.coeffs = w
+
+    def outputs(self):
+        return [self.coeffs, self.xr], "f32 MODWT rows [series, J+1, samples] + reconstruction"
 
     def check(self):
         return float((self.xr - self.x).abs().max().item() / self.x.abs().max().item())
@@ -374,6 +399,10 @@ class C4(Workload):
             self.r = self.ops.wct_morlet(self.y1, self.y2, self.sjd, DT, 6.0, boxcar=self.K,
                                          want_uv=False, want_power=True, want_phase=True,
                                          workspace=self.ws, normalize=True)
+
+    def outputs(self):
+        return [self.r["power"], self.r["coh"], self.r["phase"]], \
+            "f32 |W12|^2, WCT, phase [pairs, scales, samples]"
 
     def check(self):
         """First and last pair's coherence vs the oracle's pycwt.wct (max abs difference)."""
@@ -491,6 +520,49 @@ def step_bound(cfg, per_step, step_ms, hbm_frac):
                    source=os.path.relpath(path, ROOT))
         return out
     return out
+
+
+def measure_gather(wl, pageable=True):
+    """Host gather of this rank's output, after and outside the timed region (SURVEY 8(d)/(e):
+    "D2H into pinned buffers, timed separately"): the page-locked buffers are allocated first
+    (timed on their own: a consumer keeps them), then the copy of every output tensor into
+    them is timed, and the same copy into pageable memory beside it.  Bytes are the outputs'."""
+    import torch
+    from wtmi import sharding
+    outs, what = wl.outputs()
+    nbytes = sum(t.numel() * t.element_size() for t in outs)
+    rec = {"what": what, "bytes": nbytes}
+    if not outs or nbytes == 0:
+        return rec
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    bufs = [sharding.pinned_buffer(t.shape, t.dtype, reuse=False) for t in outs]
+    rec["pinned_alloc_ms"] = (time.perf_counter() - t0) * 1e3
+    # warm the copy path once on a small slice (first-call driver set-up is not transfer time)
+    sharding.d2h(outs[0].reshape(-1)[:1024], out=bufs[0].reshape(-1)[:1024])
+    best = None
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t, b in zip(outs, bufs):
+            sharding.d2h(t, out=b)
+        ms = (time.perf_counter() - t0) * 1e3
+        best = ms if best is None else min(best, ms)
+    rec.update(pinned_ms=best, pinned_GBps=nbytes / best / 1e6,
+               note="best of 2 copies into the same page-locked buffers; value excludes it")
+    if pageable:
+        host = [torch.empty(t.shape, dtype=t.dtype) for t in outs]
+        for h in host:  # first-touch the pages outside the clock
+            h.reshape(-1).view(torch.uint8)[::4096] = 0
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t, h in zip(outs, host):
+            h.copy_(t)
+        ms = (time.perf_counter() - t0) * 1e3
+        rec.update(pageable_ms=ms, pageable_GBps=nbytes / ms / 1e6)
+        del host
+    del bufs
+    return rec
 
 
 def pmc_traffic(cfg, per_step):
@@ -616,6 +688,8 @@ def main():
                     help="initialise the process group even at --gpus 1 (RANK 0 of WORLD_SIZE 1 on "
                          "127.0.0.1): the RCCL barrier / all-reduce / gloo side-group gather run on "
                          "one GPU")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the host-gather measurement after the timed region")
     ap.add_argument("--rank-timeout", type=float, default=0.0,
                     help="self-launched ranks: wall-clock limit in seconds (0 = none)")
     args = ap.parse_args()
@@ -752,6 +826,11 @@ def main():
     own_max, own_min = sharding.max_over_ranks(t_own), -sharding.max_over_ranks(-t_own)
     bar_max, bar_min = sharding.max_over_ranks(t_barrier), -sharding.max_over_ranks(-t_barrier)
     check = wl.check() if rank == 0 and wl.local else None
+    gather_rec = None
+    if args.device == "cuda" and not args.no_gather:
+        gather_rec = measure_gather(wl)
+        if dist_on:  # the slowest rank's copy (each rank gathers its own block)
+            gather_rec["pinned_ms_max_over_ranks"] = sharding.max_over_ranks(gather_rec.get("pinned_ms", 0.0))
     gathered = None
     if dist_on:
         # the host-side gather of sharding.gather_to_rank0 (a gloo side group under RCCL):
@@ -812,6 +891,7 @@ def main():
                       "note": "own = a rank's K steps up to its sync, before the closing barrier; "
                               "value uses the max over ranks of own + barrier"},
             "graph": bool(use_graph),
+            "gather": gather_rec,
         }
         print(json.dumps(line), flush=True)
     if dist_on:

@@ -58,8 +58,12 @@ def _rank_main(rank, world, port, out_dir):
     W, M = _transform(x[s:e])
     gW = sharding.gather_to_rank0(torch.view_as_real(W), B)
     gM = sharding.gather_to_rank0(M, B)
+    # the pageable path gathers the same bits
+    pW = sharding.gather_to_rank0(torch.view_as_real(W), B, pinned=False)
+    pM = sharding.gather_to_rank0(M, B, pinned=False)
     t = sharding.max_over_ranks(1.0 + rank)
     if rank == 0:
+        assert torch.equal(gW, pW) and torch.equal(gM, pM)
         np.save(os.path.join(out_dir, "W.npy"), torch.view_as_complex(gW).numpy())
         np.save(os.path.join(out_dir, "M.npy"), gM.numpy())
         np.save(os.path.join(out_dir, "t.npy"), np.array([t]))
@@ -165,3 +169,24 @@ def test_bench_force_dist_rccl():
     assert line["config"]["dist_gather"] == [[0.0, 1024 * 128 * 4096.0]]
     assert line["value"] > 0
     assert line["check"]["rank0_first_last_series_max_row_rel_err_vs_oracle"] < 1e-5
+    g = line["gather"]  # the host gather of rank 0's whole W, timed outside the region
+    assert g["bytes"] == 1024 * 128 * 4096 * 8
+    assert g["pinned_ms"] > 0 and g["pinned_ms_max_over_ranks"] == g["pinned_ms"]
+    print("gather", {k: g[k] for k in ("pinned_ms", "pinned_GBps", "pageable_ms", "pageable_GBps")})
+
+
+def test_pinned_d2h_bitwise_equal_to_pageable():
+    """sharding.d2h: the page-locked copy (pool buffer, reused) and the pageable copy of the
+    same device tensors hold the same bits, for a CWT output and for odd sizes / dtypes."""
+    import torch
+    from wtmi import sharding
+    W, M = _transform(_batch())
+    for t in (torch.view_as_real(W), M, M[3:7], torch.arange(12345, device="cuda", dtype=torch.int64)):
+        a = sharding.d2h(t)
+        assert a.is_pinned()
+        b = sharding.d2h(t, pinned=False)
+        assert not b.is_pinned()
+        assert torch.equal(a, b) and torch.equal(a, t.cpu())
+        sharding.release_pinned(a)
+    again = sharding.d2h(M)  # taken from the pool
+    assert torch.equal(again, M.cpu())

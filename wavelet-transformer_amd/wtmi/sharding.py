@@ -10,6 +10,13 @@ Process groups: an RCCL group (backend "nccl" on ROCm) has no CPU transport, so 
 host-side gather runs over a gloo side group created once from the same ranks
 (``host_group``), and scalar reductions use the group's own device.  Under a gloo (or
 "cpu:gloo,cuda:nccl") group everything stays on the host.
+
+Device-to-host copies ("D2H into pinned buffers, timed separately") go
+through page-locked host buffers (``d2h``): a pageable ``.to("cpu")`` stages every byte
+through a driver bounce buffer, a pinned destination is written by the DMA engine directly.
+The buffers are kept in a small per-process pool keyed by size, so a consumer that gathers
+every batch (the reference's per-series loop, src/utils/transform_helpers.py:116-135) pays
+the page-locking once.
 """
 
 from __future__ import annotations
@@ -40,6 +47,56 @@ def run_sharded(x: torch.Tensor, fn: Callable[[torch.Tensor], torch.Tensor], ran
     return fn(x[s:e])
 
 
+_PINNED: dict = {}
+_PINNED_LOCK = threading.Lock()
+PINNED_POOL_BYTES = 32 << 30  # buffers kept for reuse, at most this many bytes in total
+
+
+def pinned_buffer(shape, dtype, reuse: bool = True) -> torch.Tensor:
+    """A page-locked host tensor of `shape` / `dtype`.  With `reuse`, taken from (and later
+    returned to, by ``release_pinned``) a per-process pool keyed by byte size."""
+    shape = tuple(int(v) for v in shape)
+    nbytes = torch.Size(shape).numel() * torch.empty((), dtype=dtype).element_size()
+    if reuse:
+        with _PINNED_LOCK:
+            lst = _PINNED.get(nbytes)
+            if lst:
+                raw = lst.pop()
+                return raw.view(dtype).view(shape) if nbytes else torch.empty(shape, dtype=dtype)
+    if nbytes == 0:
+        return torch.empty(shape, dtype=dtype)
+    raw = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    return raw.view(dtype).view(shape)
+
+
+def release_pinned(t: torch.Tensor) -> None:
+    """Return a buffer from ``pinned_buffer`` to the pool (dropped if the pool is full)."""
+    if not t.is_pinned() or t.numel() == 0:
+        return
+    raw = t.reshape(-1).view(torch.uint8)
+    with _PINNED_LOCK:
+        held = sum(k * len(v) for k, v in _PINNED.items())
+        if held + raw.numel() <= PINNED_POOL_BYTES:
+            _PINNED.setdefault(raw.numel(), []).append(raw)
+
+
+def d2h(t: torch.Tensor, pinned: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Copy a device tensor to host memory and wait for it: into `out` (any host tensor of the
+    same shape and dtype), else into a pinned pool buffer (`pinned`), else a pageable one.
+    The copy runs on the current stream after the work already queued there.  A host tensor
+    is returned as is (contiguous)."""
+    if t.device.type != "cuda":
+        return t.contiguous()
+    if out is None:
+        out = pinned_buffer(t.shape, t.dtype) if pinned else torch.empty(t.shape, dtype=t.dtype)
+    if tuple(out.shape) != tuple(t.shape) or out.dtype != t.dtype:
+        raise ValueError(f"d2h: out {tuple(out.shape)} {out.dtype} for {tuple(t.shape)} {t.dtype}")
+    out.copy_(t, non_blocking=out.is_pinned())
+    if out.is_pinned():
+        torch.cuda.current_stream(t.device).synchronize()
+    return out
+
+
 def _has_cpu_transport(group) -> bool:
     return "gloo" in str(dist.get_backend(group)).lower()
 
@@ -66,28 +123,43 @@ def host_group(group=None):
     return g
 
 
-def gather_to_rank0(local: torch.Tensor, batch: int, group=None) -> Optional[torch.Tensor]:
+def gather_to_rank0(local: torch.Tensor, batch: int, group=None,
+                    pinned: bool = True) -> Optional[torch.Tensor]:
     """Host-side gather of per-rank result blocks into the global batch order on rank 0.
 
-    Each rank copies its block to host memory (D2H) and the blocks travel over a gloo
-    group (``host_group``): nothing of the data path goes through RCCL, under either
-    backend.  Returns the [batch, ...] host tensor on rank 0, None elsewhere."""
+    Each rank copies its block to host memory (D2H into a pinned buffer, ``d2h``; pageable
+    with ``pinned=False``) and the blocks travel over a gloo group (``host_group``): nothing
+    of the data path goes through RCCL, under either backend.  Rank 0 receives every block
+    straight into its slot of one [world * ceil(batch / world), ...] host tensor (no
+    concatenation copy).  Returns the [batch, ...] host tensor on rank 0, None elsewhere."""
     hg = host_group(group)
     world = dist.get_world_size(hg)
     rank = dist.get_rank(hg)
-    host = local.detach().to("cpu").contiguous()
     per = -(-batch // world)
     s, e = shard_range(batch, rank, world)
-    if host.shape[0] != e - s:
-        raise ValueError(f"rank {rank} holds {host.shape[0]} rows, its shard is {e - s}")
-    pad_shape = (per,) + tuple(host.shape[1:])
-    buf = torch.zeros(pad_shape, dtype=host.dtype)
-    buf[: host.shape[0]] = host
-    out = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, out, dst=dist.get_global_rank(hg, 0) if hg is not None else 0, group=hg)
+    if local.shape[0] != e - s:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard is {e - s}")
+    pad_shape = (per,) + tuple(local.shape[1:])
+    src = local.detach()
+    if src.shape[0] == per:
+        buf = d2h(src, pinned=pinned)
+    else:  # the last (short) block travels padded to the common block size
+        buf = torch.zeros(pad_shape, dtype=src.dtype)
+        if src.shape[0]:
+            tmp = d2h(src, pinned=pinned)
+            buf[: src.shape[0]] = tmp
+            release_pinned(tmp)
+    out = None
+    if rank == 0:
+        full = torch.empty((per * world,) + tuple(local.shape[1:]), dtype=local.dtype)
+        out = [full[r * per:(r + 1) * per] for r in range(world)]
+    dist.gather(buf.contiguous(), out, dst=dist.get_global_rank(hg, 0) if hg is not None else 0,
+                group=hg)
+    if pinned and buf.is_pinned():
+        release_pinned(buf)
     if rank != 0:
         return None
-    return torch.cat(out, dim=0)[:batch]
+    return full[:batch]
 
 
 def _reduce_device(group=None) -> torch.device:
