@@ -10,7 +10,7 @@
 #   PARTS selects the parts: "pmc prof roof bench" (default all).
 # Every GPU step has its own time limit; a crash / abort / timeout ends the session.
 set -u
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 PARTS=${PARTS:-"pmc prof roof bench"}
 CFGS=${CFGS:-"c2 c3 c4 c5"}
 OUT=gpurun_out
