@@ -28,7 +28,7 @@ has() { case " $PARTS " in *" $1 "*) return 0;; esac; return 1; }
 if has pmc; then
   for c in $CFGS; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
-      run pmc_${c}_$ctr 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/pmc_${c}_$ctr -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
+      run pmc_${c}_$ctr 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/pmc_${c}_$ctr -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-gather
     done
     python scripts/pmc_traffic.py $c $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/pmc_traffic.json > /dev/null || exit 1
   done
@@ -38,7 +38,7 @@ if has prof; then
   for c in $CFGS; do
     STEPS_K=10
     [ $c = c2 ] && STEPS_K=50
-    run prof_$c 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$c -o run -- python bench.py --config $c --steps $STEPS_K --warmup 5 --no-cpu-baseline
+    run prof_$c 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$c -o run -- python bench.py --config $c --steps $STEPS_K --warmup 5 --no-cpu-baseline --no-gather
     python scripts/trace_mean.py $OUT/prof_$c $STEPS_K > $OUT/prof_$c/timed_mean.txt
   done
 fi
@@ -46,12 +46,12 @@ if has roof; then
   for c in $CFGS; do
     TR=$OUT/prof_$c
     if [ $c = c4 ]; then  # per-kernel durations from a one-stream trace (each kernel's own time)
-      WTMI_WCT_SIDE_STREAM=0 run prof_c4_serial 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4_serial -o run -- python bench.py --config c4 --steps 10 --warmup 5 --no-cpu-baseline
+      WTMI_WCT_SIDE_STREAM=0 run prof_c4_serial 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4_serial -o run -- python bench.py --config c4 --steps 10 --warmup 5 --no-cpu-baseline --no-gather
       python scripts/trace_mean.py $OUT/prof_c4_serial 10 > $OUT/prof_c4_serial/timed_mean.txt
       TR=$OUT/prof_c4_serial
     fi
-    run valu_$c 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/valu_$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
-    run lds_$c 400 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/lds_$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline
+    run valu_$c 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/valu_$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-gather
+    run lds_$c 400 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/lds_$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-gather
     STEPS_K=10
     [ $c = c2 ] && STEPS_K=50
     python scripts/kernel_roofline.py $c $TR $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE $OUT/valu_$c $OUT/kernel_roofline.json $STEPS_K $OUT/lds_$c > $OUT/roof_$c.txt || exit 1
