@@ -496,9 +496,11 @@ def step_bound(cfg, per_step, step_ms, hbm_frac):
     import glob
     out = {"bound": "hbm", "hbm": hbm_frac, "valu": None, "valu_insts_per_step": None,
            "source": None,
-           "note": "valu = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz x step time): a model; "
-                   "transcendental ops issue at a quarter rate (undercounted) and packed FP32 ops do "
-                   "two lanes' work (overcounted relative to scalar), so read it to about +-20 %"}
+           "note": "valu = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz x step time): a model. "
+                   "MI355X_MICROARCH's measured issue costs: v_fma_f32 2 cycles per SIMD-32 with "
+                   "several waves (4 for one wave alone), transcendentals 8, so a single rate is an "
+                   "approximation; the per-kernel valu_busy (SQ_ACTIVE_INST_VALU) measured beside it "
+                   "agrees within ~10 % for the WCT kernels (e.g. 0.63 measured vs 0.57 modelled)"}
     if not per_step or not step_ms:
         return out
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_roofline.json")), reverse=True):
