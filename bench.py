@@ -529,6 +529,13 @@ def measure_gather(wl, pageable=True):
     "D2H into pinned buffers, timed separately"): the page-locked buffers are allocated first
     (timed on their own: a consumer keeps them), then the copy of every output tensor into
     them is timed, and the same copy into pageable memory beside it.  Bytes are the outputs'."""
+    try:
+        return _measure_gather(wl, pageable)
+    except Exception as e:  # a host without page-locked memory to spare must not lose the line
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def _measure_gather(wl, pageable):
     import torch
     from wtmi import sharding
     outs, what = wl.outputs()
@@ -830,7 +837,9 @@ def main():
     check = wl.check() if rank == 0 and wl.local else None
     gather_rec = None
     if args.device == "cuda" and not args.no_gather:
-        gather_rec = measure_gather(wl)
+        # the pageable comparison only at N = 1 (N ranks' pageable copies would double the host
+        # memory the gather holds)
+        gather_rec = measure_gather(wl, pageable=world == 1)
         if dist_on:  # the slowest rank's copy (each rank gathers its own block)
             gather_rec["pinned_ms_max_over_ranks"] = sharding.max_over_ranks(gather_rec.get("pinned_ms", 0.0))
     gathered = None
