@@ -70,3 +70,20 @@ def test_shard_range_covers_batch_once():
                 s, e = shard_range(batch, r, world)
                 seen.extend(range(s, e))
             assert seen == list(range(batch))
+
+
+def test_pinned_pool_reuse_and_host_passthrough():
+    """sharding.pinned_buffer reuses released buffers by size; d2h of a host tensor returns it
+    as is (never a pool buffer), so gather_to_rank0 of host blocks cannot pool the caller's
+    memory."""
+    import torch
+    from wtmi import sharding
+    x = torch.arange(12, dtype=torch.float32).reshape(3, 4)
+    assert sharding.d2h(x) is x
+    if not torch.cuda.is_available():
+        return
+    a = sharding.pinned_buffer((3, 4), torch.float32)
+    ptr = a.data_ptr()
+    sharding.release_pinned(a)
+    b = sharding.pinned_buffer((4, 3), torch.float32)
+    assert b.data_ptr() == ptr and b.is_pinned()

@@ -70,7 +70,8 @@ def pinned_buffer(shape, dtype, reuse: bool = True) -> torch.Tensor:
 
 
 def release_pinned(t: torch.Tensor) -> None:
-    """Return a buffer from ``pinned_buffer`` to the pool (dropped if the pool is full)."""
+    """Return a buffer from ``pinned_buffer`` (or ``d2h`` without ``out``) to the pool (dropped
+    if the pool is full).  Only such buffers may be released: the pool hands them out again."""
     if not t.is_pinned() or t.numel() == 0:
         return
     raw = t.reshape(-1).view(torch.uint8)
@@ -141,6 +142,8 @@ def gather_to_rank0(local: torch.Tensor, batch: int, group=None,
         raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard is {e - s}")
     pad_shape = (per,) + tuple(local.shape[1:])
     src = local.detach()
+    # pool buffers only come from device blocks (a host block is used as it is, never pooled)
+    pooled = pinned and src.device.type == "cuda"
     if src.shape[0] == per:
         buf = d2h(src, pinned=pinned)
     else:  # the last (short) block travels padded to the common block size
@@ -148,14 +151,16 @@ def gather_to_rank0(local: torch.Tensor, batch: int, group=None,
         if src.shape[0]:
             tmp = d2h(src, pinned=pinned)
             buf[: src.shape[0]] = tmp
-            release_pinned(tmp)
+            if pooled:
+                release_pinned(tmp)
+        pooled = False
     out = None
     if rank == 0:
         full = torch.empty((per * world,) + tuple(local.shape[1:]), dtype=local.dtype)
         out = [full[r * per:(r + 1) * per] for r in range(world)]
     dist.gather(buf.contiguous(), out, dst=dist.get_global_rank(hg, 0) if hg is not None else 0,
                 group=hg)
-    if pinned and buf.is_pinned():
+    if pooled:
         release_pinned(buf)
     if rank != 0:
         return None
